@@ -1,0 +1,214 @@
+/*
+ * oracle.c — TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Serial C restatement of the reference's canonical integer forward pass.  Each function cites
+ * the reference lines it follows (paths relative to /root/reference/edge-eegnet_wolf).
+ * Arithmetic: int32 accumulators, C '/' (truncation toward zero), '>>' arithmetic shift,
+ * clip to [-128, 127] (__CLIP_R(x, 127) of the PULP SDK, clip_balanced=False in the golden model).
+ */
+#include "oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define L2_TAPS 64
+#define L2_PAD_START 31 /* gen_net_header.py:142 */
+#define L2_PAD_END 32   /* gen_net_header.py:143 */
+#define L3_TAPS 16
+#define L3_PAD_START 7 /* gen_net_header.py:162 */
+#define L3_PAD_END 8   /* gen_net_header.py:163 */
+
+static inline int32_t clip8(int32_t v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+
+/* func_dotp (func/dotp.c:45 NO_SIMD variant): plain int8 dot product into int32 */
+static inline int32_t dotp(const int8_t* a, const int8_t* b, int len) {
+    int32_t acc = 0;
+    for (int i = 0; i < len; i++) acc += (int32_t)a[i] * (int32_t)b[i];
+    return acc;
+}
+
+/* Layer 1: layer1.c:53-101 (_net_layer1_kernel) — per filter, per time sample:
+ * y[f][t] = clip((dotp(x[t], W1[f], C_ALIGN) + off[f]) / fac[f]) */
+void or_layer1(const or_params_t* p, const int8_t* x, int8_t* y1) {
+    memset(y1, 0, (size_t)p->F1 * p->T_ALIGN);
+    for (int f = 0; f < p->F1; f++) {
+        const int8_t* w = p->l1_weight_align + (size_t)f * p->C_ALIGN;
+        int32_t fac = p->l1_factor[f], off = p->l1_offset[f];
+        for (int t = 0; t < p->T; t++) {
+            int32_t e = dotp(x + (size_t)t * p->C_ALIGN, w, p->C_ALIGN);
+            e = (e + off) / fac;
+            y1[(size_t)f * p->T_ALIGN + t] = (int8_t)clip8(e);
+        }
+    }
+}
+
+/* Layer 2, REORDER_BN branch: layer2.c:56-118 (kernel) and :231-326 (driver).
+ * Row padded with 31 leading / 32 trailing zeros (:262-275), func_xcorr with the torch-order
+ * weights net_l2_weight_reverse (xcorr.c:44: r[i] = sum_j a[i+j] * b[j]), then for each of the
+ * T/8 output samples: sum_{8} max(a, -(off >> 3)), + off, / fac, clip (:97-117). */
+void or_layer2(const or_params_t* p, const int8_t* y1, int8_t* y2) {
+    const int pad_len = p->T + L2_PAD_START + L2_PAD_END;
+    int8_t* row = (int8_t*)calloc((size_t)pad_len, 1);
+    int32_t* xc = (int32_t*)malloc(sizeof(int32_t) * (size_t)(pad_len - L2_TAPS + 1));
+    memset(y2, 0, (size_t)p->F2 * p->T8_ALIGN);
+    for (int f = 0; f < p->F2; f++) {
+        memset(row, 0, (size_t)pad_len);
+        memcpy(row + L2_PAD_START, y1 + (size_t)f * p->T_ALIGN, (size_t)p->T);
+        const int8_t* w = p->l2_weight_reverse + (size_t)f * L2_TAPS;
+        const int n_out = pad_len - L2_TAPS + 1; /* == T */
+        for (int i = 0; i < n_out; i++) {
+            int32_t acc = 0;
+            for (int j = 0; j < L2_TAPS; j++) acc += (int32_t)row[i + j] * (int32_t)w[j];
+            xc[i] = acc;
+        }
+        const int32_t fac = p->l2_factor[f], off = p->l2_offset[f];
+        const int32_t thr = -(off >> 3);
+        const int32_t* it = xc;
+        for (int u = 0; u < p->T8; u++) {
+            int32_t sum = 0;
+            for (int k = 0; k < 8; k++) {
+                int32_t v = *(it++);
+                sum += v > thr ? v : thr; /* __MAX */
+            }
+            sum = sum + off;
+            sum = sum / fac;
+            y2[(size_t)f * p->T8_ALIGN + u] = (int8_t)clip8(sum);
+        }
+    }
+    free(xc);
+    free(row);
+}
+
+/* Layer 3: layer3.c:49-79 (kernel) + :100-159 (driver).  Row padded 7/8 (:122-131),
+ * func_conv_scale(row, 155, net_l3_weight[f], 16, NET_L3_FACTOR, 0) — a TRUE convolution
+ * (conv.c:105-146: acc = offset + sum_i a[i_out+i] * b[len-1-i]; acc / div; clip). */
+void or_layer3(const or_params_t* p, const int8_t* y2, int8_t* y3) {
+    const int pad_len = p->T8 + L3_PAD_START + L3_PAD_END;
+    int8_t* row = (int8_t*)calloc((size_t)pad_len, 1);
+    memset(y3, 0, (size_t)p->F2 * p->T8_ALIGN);
+    for (int f = 0; f < p->F2; f++) {
+        memset(row, 0, (size_t)pad_len);
+        memcpy(row + L3_PAD_START, y2 + (size_t)f * p->T8_ALIGN, (size_t)p->T8);
+        const int8_t* w = p->l3_weight + (size_t)f * L3_TAPS;
+        const int n_out = pad_len - L3_TAPS + 1; /* == T8 */
+        for (int i = 0; i < n_out; i++) {
+            int32_t acc = 0; /* offset argument is 0 (layer3.c:70) */
+            for (int j = 0; j < L3_TAPS; j++) acc += (int32_t)row[i + j] * (int32_t)w[L3_TAPS - 1 - j];
+            acc = acc / p->l3_factor;
+            y3[(size_t)f * p->T8_ALIGN + i] = (int8_t)clip8(acc);
+        }
+    }
+    free(row);
+}
+
+/* net_layer3_flip_inplace: layer3.c:243-268 -> func_flip_2d_axis (flip.c:92):
+ * [F2][T8_ALIGN] -> [T8][F2] */
+void or_layer3_flip_inplace(const or_params_t* p, int8_t* y3) {
+    int8_t* tmp = (int8_t*)malloc((size_t)p->F2 * p->T8_ALIGN);
+    memcpy(tmp, y3, (size_t)p->F2 * p->T8_ALIGN);
+    memset(y3, 0, (size_t)p->F2 * p->T8_ALIGN);
+    for (int f = 0; f < p->F2; f++)
+        for (int u = 0; u < p->T8; u++) y3[(size_t)u * p->F2 + f] = tmp[(size_t)f * p->T8_ALIGN + u];
+    free(tmp);
+}
+
+/* Layer 4, FLIP_LAYERS + REORDER_BN: layer4.c:51-149.  For each output filter k and each of the
+ * T64 pooled samples: sum_{8} max(dotp(x[t], W4[k], F2), -(off >> 3)); + off; / fac; clip. */
+void or_layer4(const or_params_t* p, const int8_t* y3t, int8_t* y4) {
+    memset(y4, 0, (size_t)p->F2 * p->T64_ALIGN);
+    for (int k = 0; k < p->F2; k++) {
+        const int32_t fac = p->l4_factor[k], off = p->l4_offset[k];
+        const int32_t thr = -(off >> 3);
+        const int8_t* w = p->l4_weight + (size_t)k * p->F2;
+        const int8_t* it = y3t;
+        for (int v = 0; v < p->T64; v++) {
+            int32_t sum = 0;
+            for (int i = 0; i < 8; i++) {
+                int32_t e = dotp(it, w, p->F2);
+                e = e > thr ? e : thr;
+                sum += e;
+                it += p->F2;
+            }
+            sum = sum + off;
+            sum = sum / fac;
+            y4[(size_t)k * p->T64_ALIGN + v] = (int8_t)clip8(sum);
+        }
+    }
+}
+
+/* Layer 5: layer5.c:43-89.  z[n] = dotp(y4, W5[n], F2*T64_ALIGN) + bias[n] (the weight's pad
+ * positions are zero), then func_transform_32to8 (transform.c:47-121): z / NET_L5_FACTOR, clip. */
+void or_layer5(const or_params_t* p, const int8_t* y4, int8_t* out) {
+    const int len = p->F2 * p->T64_ALIGN;
+    int8_t* xin = (int8_t*)malloc((size_t)len);
+    /* the reference leaves the T64..T64_ALIGN tail of each row uninitialised; the weight is zero
+     * there, so zero it for a deterministic product */
+    for (int k = 0; k < p->F2; k++)
+        for (int v = 0; v < p->T64_ALIGN; v++)
+            xin[k * p->T64_ALIGN + v] = v < p->T64 ? y4[(size_t)k * p->T64_ALIGN + v] : 0;
+    for (int n = 0; n < p->N; n++) {
+        int32_t z = dotp(xin, p->l5_weight + (size_t)n * len, len) + (int32_t)p->l5_bias[n];
+        z = z / p->l5_factor;
+        out[n] = (int8_t)clip8(z);
+    }
+    free(xin);
+}
+
+/* net_model_compute: model.c:84-148 */
+void or_model_compute(const or_params_t* p, const int8_t* x, int8_t* out) {
+    int8_t* y1 = (int8_t*)malloc((size_t)p->F1 * p->T_ALIGN);
+    int8_t* y2 = (int8_t*)malloc((size_t)p->F2 * p->T8_ALIGN);
+    int8_t* y3 = (int8_t*)malloc((size_t)p->F2 * p->T8_ALIGN);
+    int8_t* y4 = (int8_t*)malloc((size_t)p->F2 * p->T64_ALIGN);
+    or_layer1(p, x, y1);
+    or_layer2(p, y1, y2);
+    or_layer3(p, y2, y3);
+    or_layer3_flip_inplace(p, y3);
+    or_layer4(p, y3, y4);
+    or_layer5(p, y4, out);
+    free(y1); free(y2); free(y3); free(y4);
+}
+
+typedef struct {
+    const or_params_t* p;
+    const int8_t* x;
+    size_t stride;
+    int8_t* out;
+    size_t b0, b1;
+} or_job_t;
+
+static void* or_worker(void* arg) {
+    or_job_t* j = (or_job_t*)arg;
+    const or_params_t* p = j->p;
+    int8_t* xa = (int8_t*)calloc((size_t)p->T * p->C_ALIGN, 1);
+    for (size_t b = j->b0; b < j->b1; b++) {
+        const int8_t* xt = j->x + b * j->stride;
+        for (int t = 0; t < p->T; t++)
+            memcpy(xa + (size_t)t * p->C_ALIGN, xt + (size_t)t * p->C, (size_t)p->C);
+        or_model_compute(p, xa, j->out + b * (size_t)p->N);
+    }
+    free(xa);
+    return NULL;
+}
+
+void or_model_compute_batch(const or_params_t* p, const int8_t* x, size_t trial_stride,
+                            int8_t* out, size_t B, int nthreads) {
+    if (nthreads <= 1 || B < 2) {
+        or_job_t j = {p, x, trial_stride, out, 0, B};
+        or_worker(&j);
+        return;
+    }
+    if ((size_t)nthreads > B) nthreads = (int)B;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    or_job_t* jobs = (or_job_t*)malloc(sizeof(or_job_t) * (size_t)nthreads);
+    for (int i = 0; i < nthreads; i++) {
+        jobs[i].p = p; jobs[i].x = x; jobs[i].stride = trial_stride; jobs[i].out = out;
+        jobs[i].b0 = B * (size_t)i / (size_t)nthreads;
+        jobs[i].b1 = B * (size_t)(i + 1) / (size_t)nthreads;
+        pthread_create(&th[i], NULL, or_worker, &jobs[i]);
+    }
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    free(th);
+    free(jobs);
+}
