@@ -1,0 +1,189 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X int8 MI-BMInet forward (BASELINE.json metric).
+
+One "step" = one fused forward pass (one kernel launch) over a batch of 65,536 synthetic
+22-channel x 1125-sample int8 trials already resident in HBM (BASELINE config B; with --gpus N
+each rank owns its own 65,536-trial shard: config E's static split, weak scaling, no collectives).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config b22|c64|d22] [--batch B]
+
+For N > 1 launch under ``torch.distributed.run`` (one process per GPU); rank 0 prints ONE JSON
+line.  ``value`` = trials processed by all ranks / max-over-ranks wall time of the K timed steps.
+``roofline.achieved`` = algorithmic bytes per launch (input 22*1125 B + 4 B logits per trial) /
+average kernel duration from HIP events on the launch stream.  ``cpu_baseline`` times the C
+restatement of the reference forward (oracle/, kind "port") on the host cores (rank 0, N = 1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mi-bminet_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mibminet import lib  # noqa: E402
+from mibminet.params import ParamSet  # noqa: E402
+
+METRIC = "EEG trials/sec (int8, 22ch×1125) at batch 65536; bit-exact logits"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+CONFIGS = {
+    "b22": dict(C=22, T=1125, wbits=8, name="B: 22ch x 1125 int8, 4-class"),
+    "c64": dict(C=64, T=1000, wbits=8, name="C: 64ch x 1000 int8, 4-class"),
+    "d22": dict(C=22, T=1125, wbits=4, name="D: 22ch x 1125, int4 weights / int8 acts"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=65536, help="trials per GPU")
+    ap.add_argument("--config", default="b22", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline wall time")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(ps, x_dev, seconds):
+    """Times the oracle's C restatement of net_model_compute on a bounded sample of the same
+    workload, trials split over the host threads this process may use (rank 0, N = 1 only)."""
+    sys.path.insert(0, ROOT)
+    import oracle  # test infrastructure: only this leg of bench.py may use it
+
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", ncpu)), ncpu, 16))
+    co = oracle.COracle(ps)
+    calib = x_dev[: 4 * threads].cpu().numpy()
+    t0 = time.perf_counter()
+    co.batch(calib, nthreads=threads)
+    dt = max(time.perf_counter() - t0, 1e-6)
+    per_trial = dt / calib.shape[0]
+    n = int(min(x_dev.shape[0], max(8 * threads, seconds / per_trial)))
+    sample = x_dev[:n].cpu().numpy()
+    t0 = time.perf_counter()
+    co.batch(sample, nthreads=threads)
+    dt = time.perf_counter() - t0
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
+            "sample": f"{n} trials of the same synthetic batch, C restatement (oracle/oracle.c, -O3) "
+                      f"of net_model_compute, {threads} host threads on {cpu}, {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    cfg = CONFIGS[a.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    ps = ParamSet.synthetic(seed=a.seed, C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"])
+    lib.params_load(ps)
+    stride = lib.trial_stride()
+    B = a.batch
+    g = torch.Generator(device=dev)
+    g.manual_seed(a.seed * 1000 + rank)
+    x = torch.randint(-128, 128, (B, stride), dtype=torch.int8, device=dev, generator=g)
+    x[:, cfg["C"] * cfg["T"]:] = 0
+    y = torch.empty((B, 4), dtype=torch.int8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step():
+        lib.model_compute_batch(x.data_ptr(), y.data_ptr(), B, local, sp)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [s.elapsed_time(e) for s, e in ev]
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    info = lib.launch_info(B, local)
+    if rank == 0:
+        avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+        alg_bytes_trial = cfg["C"] * cfg["T"] + 4
+        achieved = alg_bytes_trial * B / avg_kernel_s / 1e9
+        traffic = None
+        try:
+            tj = json.load(open(a.traffic_json))
+            if tj.get("config") == a.config and tj.get("batch") == B:
+                traffic = tj["hbm_bytes_per_launch"]
+        except (OSError, ValueError, KeyError):
+            pass
+        value = world * B * a.steps / elapsed
+        out = {
+            "metric": METRIC if a.config == "b22" else f"EEG trials/sec ({cfg['name']}) at batch {B}",
+            "value": value,
+            "unit": "trials/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8",
+            "data": "synthetic (uniform int8 EEG generated on device; seeded synthetic integer weights)",
+            "config": {"workload": cfg["name"], "C": cfg["C"], "T": cfg["T"], "batch_per_gpu": B,
+                       "global_batch": world * B, "weight_bits": cfg["wbits"],
+                       "parallelism": f"dp{world} static batch split, no collectives",
+                       "grid": info["grid"], "threads": info["threads"], "lds_bytes": info["lds_bytes"]},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_forward<Cfg<%d,%d>>" % (cfg["C"], cfg["T"]),
+                         "avg_kernel_ms": avg_kernel_s * 1e3,
+                         "alg_bytes_per_launch": alg_bytes_trial * B},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(ps, x, a.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,111 @@
+/*
+ * mibminet.h — C ABI of the MI355X-native int8 MI-BMInet (edgeEEGNet) inference path.
+ *
+ * Drop-in for the reference's model/layer call API (pulp-platform/MI-BMInet,
+ * edge-eegnet_wolf/src/cl/net/model.h and layers.h): same symbols, same argument meaning and the
+ * same single-trial buffer layouts, backed by hand-written CDNA4 (gfx950) HIP kernels.  Everything
+ * the reference links in as generated C globals (src/cl/net/net.{h,c}) is loaded at run time from
+ * a versioned parameter blob instead (net_params_load).
+ *
+ * Layout conventions (reference layouts, "_ALIGN" = rounded up to a multiple of 4):
+ *   input       [T][C_ALIGN]   int8   (model.h:37 / model.c:81, gen_input_header.py:74-75)
+ *   layer1 out  [F1][T_ALIGN]  int8   (layer1.c:116)
+ *   layer2 out  [F2][T8_ALIGN] int8   (layer2.c:225)
+ *   layer3 out  [F2][T8_ALIGN] int8   (layer3.c:95), [T8][F2] after net_layer3_flip_inplace
+ *   layer4 out  [F2][T64_ALIGN] int8  (layer4.c:168)
+ *   output      [N]            int8   (model.h:38)
+ * Padding bytes of every produced buffer are written as zero.
+ *
+ * Batched layout (net_model_compute_batch): trial b starts at x + b * net_trial_stride(); each
+ * trial is time-major [T][C] without channel padding, trial stride = C*T rounded up to 16 bytes.
+ * Output is [B][N] int8.  Both pointers are DEVICE pointers on `device`.
+ *
+ * Errors: functions returning int return NET_OK (0) or a negative code; the reference's void
+ * entry points keep their void signature and record the status for net_last_error().
+ * Thread safety: every entry point may be called from any host thread; calls on one device are
+ * serialised internally, different devices run concurrently.
+ */
+#ifndef MIBMINET_H
+#define MIBMINET_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIBMINET_VERSION 1
+
+#define NET_OK 0
+#define NET_ERR_INVALID (-1)     /* bad argument (null pointer, bad size, bad device) */
+#define NET_ERR_NO_PARAMS (-2)   /* no parameter blob loaded */
+#define NET_ERR_UNSUPPORTED (-3) /* network dimensions without a compiled gfx950 kernel */
+#define NET_ERR_BLOB (-4)        /* malformed parameter blob */
+#define NET_ERR_RANGE (-5)       /* parameters outside the exactly-representable envelope */
+#define NET_ERR_HIP (-100)       /* HIP runtime error: code = NET_ERR_HIP - hipError_t */
+
+/* ---- reference entry points (host pointers, single trial) -------------------------------- */
+
+/* edge-eegnet_wolf/src/cl/net/model.h:40 — whole forward pass of one trial.
+ * p_data: [T][C_ALIGN] int8, p_output: [N] int8 (host memory). */
+void net_model_compute(const int8_t* p_data, int8_t* p_output);
+
+/* north_star name for the same entry, with a status return. */
+int net_forward(const int8_t* p_data, int8_t* p_output);
+
+/* edge-eegnet_wolf/src/cl/net/layers.h:46 (layer1.c:121): [T][C_ALIGN] -> [F1][T_ALIGN] */
+void net_layer1(const int8_t* p_data, int8_t* p_result);
+/* layers.h:74 (layer2.c:228): [F1][T_ALIGN] -> [F2][T8_ALIGN] */
+void net_layer2(const int8_t* p_data, int8_t* p_result);
+/* layers.h:97 (layer3.c:98): [F2][T8_ALIGN] -> [F2][T8_ALIGN] */
+void net_layer3(const int8_t* p_data, int8_t* p_result);
+/* layers.h:107 (layer3.c:243): [F2][T8_ALIGN] -> [T8][F2] in place */
+void net_layer3_flip_inplace(int8_t* p_data);
+/* layers.h:123 (layer4.c:172, FLIP_LAYERS): [T8][F2] -> [F2][T64_ALIGN] */
+void net_layer4(const int8_t* p_data, int8_t* p_result);
+/* layers.h:134 (layer5.c:43): [F2][T64_ALIGN] -> [N] */
+void net_layer5(const int8_t* p_data, int8_t* p_result);
+
+/* Status of the last void entry point called on this host thread. */
+int net_last_error(void);
+
+/* ---- parameters (replace the link-time globals of the generated net.h/net.c) ------------- */
+
+/* Load a parameter blob (format: mi-bminet_amd/mibminet/params.py, ParamSet.to_blob): the
+ * net.h arrays net_l1_factor ... net_l5_weight with their dimensions, int8 or packed int4
+ * weights.  Validates, precomputes the gfx950 operand fragments and exact requantisation
+ * reciprocals, and uploads lazily to each device on first use.  Replaces any previous set. */
+int net_params_load(const void* blob, size_t len);
+
+/* dims[0..6] = C, T, F1, F2, N, weight_bits, loaded(0/1). */
+int net_params_dims(int32_t* dims);
+
+void net_params_unload(void);
+
+/* ---- batched device entry points ---------------------------------------------------------- */
+
+/* Bytes between consecutive trials of the batched input for the loaded network (0 if none). */
+size_t net_trial_stride(void);
+
+/* Forward B trials resident on `device`; x: device pointer [B][trial_stride], y: device pointer
+ * [B][N].  Launches on the device's null stream and waits for completion. */
+int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device);
+
+/* Same, enqueued on `stream` (a hipStream_t of `device`, NULL = null stream), no host sync. */
+int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream);
+
+/* Device used by the single-trial API (default 0). */
+int net_set_device(int device);
+
+/* Kernel launch geometry used for a batch of B trials (for profiling/roofline bookkeeping):
+ * out[0] = grid size (workgroups), out[1] = threads per workgroup, out[2] = LDS bytes. */
+int net_launch_info(size_t B, int device, int32_t* out);
+
+const char* net_error_string(int code);
+int net_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIBMINET_H */

@@ -1,0 +1,549 @@
+// mibminet.hip — host side of libmibminet.so: the C ABI declared in include/mibminet.h.
+//
+// * parses the parameter blob (mibminet/params.py, ParamSet.to_blob) holding the reference's
+//   net.h arrays (edge-eegnet_wolf/data/gen_net_header.py:91-224),
+// * builds the gfx950 operand fragments and exact requantisation reciprocals (DevParams),
+// * uploads them lazily per device and dispatches the compiled (C, T) instantiations of the
+//   kernels in forward.hpp.
+// There is no CPU compute path: without a usable HIP device every entry point returns an error.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/mibminet.h"
+#include "forward.hpp"
+
+using namespace mib;
+
+namespace {
+
+constexpr int MAX_DEVICES = 64;
+constexpr int HEADER_SIZE = 64;
+constexpr uint32_t FLAG_REORDER_BN = 1;
+
+struct Dims {
+  int C = 0, T = 0, F1 = 0, F2 = 0, D = 0, N = 0, wbits = 8;
+  int C_ALIGN() const { return (C + 3) & ~3; }
+  int T_ALIGN() const { return (T + 3) & ~3; }
+  int T8() const { return T / 8; }
+  int T8_ALIGN() const { return (T8() + 3) & ~3; }
+  int T64() const { return T8() / 8; }
+  int T64_ALIGN() const { return (T64() + 3) & ~3; }
+};
+
+// Host copy of the net.h arrays (weights unpacked to int8).
+struct HostParams {
+  Dims d;
+  std::vector<int32_t> l1_factor, l1_offset, l2_factor, l2_offset, l4_factor, l4_offset;
+  std::vector<int8_t> l1_weight_align, l2_weight_reverse, l3_weight, l4_weight, l5_bias, l5_weight;
+  int32_t l3_factor = 0, l5_factor = 0;
+};
+
+// ---- exact requantisation ------------------------------------------------------------------
+// y = clip(trunc(v / fac), -128, 127) is computed on the GPU as clip((int)((float)v * r)).
+// (float)v is exact for |v| < 2^24 and (int) truncates toward zero.  q(v) = (int)RN(v * r) is
+// monotone in v, so it equals trunc(v / fac) on a whole constant interval of trunc(v / fac) iff it
+// does at both ends.  verify() checks both ends of the intervals for k = -129 .. 128, which pins
+// the clipped result for every v.  choose_reciprocal() starts at |1/fac| * (1 + 2^-22) (so that
+// exact multiples never round below the step) and nudges upward until verify() passes.
+
+inline int64_t trunc_div(int64_t a, int64_t b) { return a / b; }  // C semantics
+
+inline int64_t qf(int64_t v, float r) { return (int64_t)(int32_t)((float)v * r); }
+
+bool verify_reciprocal(int32_t fac, float r) {
+  const int64_t F = fac < 0 ? -(int64_t)fac : (int64_t)fac;
+  for (int64_t k = -129; k <= 128; k++) {
+    // interval of v (for |fac|) with trunc(v / F) == k
+    int64_t lo, hi;
+    if (k > 0) { lo = k * F; hi = k * F + F - 1; }
+    else if (k == 0) { lo = -(F - 1); hi = F - 1; }
+    else { lo = k * F - (F - 1); hi = k * F; }
+    if (fac < 0) {  // trunc(v / fac) = trunc(-v / F): result k on the mirrored interval -[lo, hi]
+      const int64_t a = -hi, b = -lo;
+      lo = a; hi = b;
+    }
+    const int64_t want = k;
+    if (std::llabs(lo) >= (1 << 24) || std::llabs(hi) >= (1 << 24)) return false;
+    if (qf(lo, r) != want || qf(hi, r) != want) return false;
+    if (trunc_div(lo, fac) != want || trunc_div(hi, fac) != want) return false;  // self-check
+  }
+  return true;
+}
+
+bool choose_reciprocal(int32_t fac, float* out) {
+  if (fac == 0) return false;
+  const double F = std::fabs((double)fac);
+  const double target = (1.0 / F) * (1.0 + std::ldexp(1.0, -22));
+  float r = (float)target;
+  if ((double)r < target) r = std::nextafterf(r, INFINITY);
+  for (int tries = 0; tries < 256; tries++) {
+    const float rs = fac < 0 ? -r : r;
+    if (verify_reciprocal(fac, rs)) { *out = rs; return true; }
+    r = std::nextafterf(r, INFINITY);
+  }
+  return false;
+}
+
+// ---- blob parsing ------------------------------------------------------------------------
+struct Reader {
+  const uint8_t* p;
+  size_t n, pos;
+  bool ok = true;
+  const uint8_t* take(size_t bytes) {
+    if (!ok || pos + bytes > n) { ok = false; return nullptr; }
+    const uint8_t* r = p + pos;
+    pos += bytes + ((4 - bytes % 4) % 4);
+    if (pos > n) { ok = false; return nullptr; }
+    return r;
+  }
+  std::vector<int32_t> i32(size_t count) {
+    std::vector<int32_t> v(count);
+    const uint8_t* s = take(4 * count);
+    if (s) std::memcpy(v.data(), s, 4 * count);
+    return v;
+  }
+  std::vector<int8_t> w(size_t count, int wbits) {
+    std::vector<int8_t> v(count);
+    if (wbits == 8) {
+      const uint8_t* s = take(count);
+      if (s) std::memcpy(v.data(), s, count);
+    } else {
+      const uint8_t* s = take((count + 1) / 2);
+      if (s)
+        for (size_t i = 0; i < count; i++) {
+          int nib = (s[i / 2] >> (4 * (i & 1))) & 0xF;
+          v[i] = (int8_t)(nib >= 8 ? nib - 16 : nib);
+        }
+    }
+    return v;
+  }
+  std::vector<int8_t> i8(size_t count) {
+    std::vector<int8_t> v(count);
+    const uint8_t* s = take(count);
+    if (s) std::memcpy(v.data(), s, count);
+    return v;
+  }
+};
+
+int parse_blob(const void* blob, size_t len, HostParams& hp) {
+  if (!blob || len < (size_t)HEADER_SIZE) return NET_ERR_BLOB;
+  const uint8_t* b = (const uint8_t*)blob;
+  if (std::memcmp(b, "MIBMINET", 8) != 0) return NET_ERR_BLOB;
+  uint32_t h[11];
+  std::memcpy(h, b + 8, sizeof(h));
+  const uint32_t version = h[0];
+  Dims d;
+  d.C = (int)h[1]; d.T = (int)h[2]; d.F1 = (int)h[3]; d.F2 = (int)h[4]; d.D = (int)h[5];
+  d.N = (int)h[6]; d.wbits = (int)h[7];
+  const uint32_t l2t = h[8], l3t = h[9], flags = h[10];
+  if (version != 1 || l2t != 64 || l3t != 16) return NET_ERR_BLOB;
+  if (!(flags & FLAG_REORDER_BN)) return NET_ERR_UNSUPPORTED;
+  if (d.wbits != 8 && d.wbits != 4) return NET_ERR_BLOB;
+  if (d.C <= 0 || d.T < 64 || d.F1 <= 0 || d.N <= 0 || d.F2 != d.F1 * d.D) return NET_ERR_BLOB;
+  Reader r{b, len, (size_t)HEADER_SIZE};
+  const int F2 = d.F2;
+  hp.d = d;
+  hp.l1_factor = r.i32(F2); hp.l1_offset = r.i32(F2);
+  hp.l1_weight_align = r.w((size_t)F2 * d.C_ALIGN(), d.wbits);
+  hp.l2_factor = r.i32(F2); hp.l2_offset = r.i32(F2);
+  hp.l2_weight_reverse = r.w((size_t)F2 * 64, d.wbits);
+  hp.l3_factor = r.i32(1)[0];
+  hp.l3_weight = r.w((size_t)F2 * 16, d.wbits);
+  hp.l4_factor = r.i32(F2); hp.l4_offset = r.i32(F2);
+  hp.l4_weight = r.w((size_t)F2 * F2, d.wbits);
+  hp.l5_factor = r.i32(1)[0];
+  hp.l5_bias = r.i8(d.N);
+  hp.l5_weight = r.w((size_t)d.N * F2 * d.T64_ALIGN(), d.wbits);
+  if (!r.ok || r.pos != len) return NET_ERR_BLOB;
+  return NET_OK;
+}
+
+// ---- device parameter image --------------------------------------------------------------
+int build_devparams(const HostParams& hp, DevParams& dp) {
+  const Dims& d = hp.d;
+  if (d.F1 != F2 || d.F2 != F2 || d.N != N_OUT) return NET_ERR_UNSUPPORTED;
+  if (d.C > 64) return NET_ERR_UNSUPPORTED;
+  const int P = d.C <= 32 ? 2 : 1;
+  const int C = d.C, CA = d.C_ALIGN();
+  std::memset(&dp, 0, sizeof(dp));
+  auto w1 = [&](int f, int c) -> int { return hp.l1_weight_align[(size_t)f * CA + c]; };
+  // value ranges for the float paths (|value| < 2^22 for the magic-offset trick, 2^24 otherwise)
+  const int64_t A = 128 * 128;
+  for (int f = 0; f < F2; f++) {
+    if (std::llabs((int64_t)hp.l1_offset[f]) + (int64_t)C * A >= (1 << 22)) return NET_ERR_RANGE;
+    if (std::llabs((int64_t)hp.l2_offset[f]) + 8LL * 64 * A >= (1 << 24)) return NET_ERR_RANGE;
+    if (std::llabs((int64_t)hp.l4_offset[f]) + 8LL * F2 * A >= (1 << 24)) return NET_ERR_RANGE;
+  }
+  if (128LL + (int64_t)F2 * d.T64() * A >= (1 << 24)) return NET_ERR_RANGE;
+  // layer 1: B operand (column j of N-tile t: filter 8t + j/2, parity j&1 when P == 2)
+  for (int t = 0; t < P; t++) {
+    for (int lane = 0; lane < 64; lane++) {
+      const int j = lane & 15, g = lane >> 4;
+      const int f = P == 2 ? 8 * t + (j >> 1) : j;
+      const int p = P == 2 ? (j & 1) : 0;
+      int8_t bytes[16];
+      for (int jj = 0; jj < 16; jj++) {
+        const int k = 16 * g + jj;  // byte of the 64-byte window
+        const int c = k - C * p;    // channel of sample p in the window
+        bytes[jj] = (int8_t)((c >= 0 && c < C) ? w1(f, c) : 0);
+      }
+      std::memcpy(&dp.l1_wfrag[t][lane], bytes, 16);
+    }
+    for (int j = 0; j < 16; j++) {
+      const int f = P == 2 ? 8 * t + (j >> 1) : j;
+      dp.l1_cinit[t][j] = hp.l1_offset[f] + FMAGIC_I;
+      if (!choose_reciprocal(hp.l1_factor[f], &dp.l1_r[t][j])) return NET_ERR_RANGE;
+    }
+  }
+  // layer 2: A operand = banded weights; row i <-> shift n(i) so that lane (c, h) register r
+  // holds output shift 16h + r (two complete pool-8 windows per lane).
+  for (int f = 0; f < F2; f++) {
+    for (int s = 0; s < 3; s++)
+      for (int lane = 0; lane < 64; lane++) {
+        const int i = lane & 31, hh = lane >> 5;
+        const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
+        int8_t bytes[16];
+        for (int jj = 0; jj < 16; jj++) {
+          const int kp = 32 * s + 16 * hh + jj;  // position in the 96-byte row window
+          const int idx = kp - n - 1;            // tap (torch order)
+          bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
+        }
+        std::memcpy(&dp.l2_afrag[f][s][lane], bytes, 16);
+      }
+    dp.l2_thr[f] = -(hp.l2_offset[f] >> 3);
+    dp.l2_off[f] = hp.l2_offset[f];
+    if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f])) return NET_ERR_RANGE;
+  }
+  SmallParams& sp = dp.sp;
+  // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed
+  for (int f = 0; f < F2; f++) {
+    int8_t taps[16];
+    for (int j = 0; j < 16; j++) taps[j] = hp.l3_weight[(size_t)f * 16 + 15 - j];
+    std::memcpy(sp.l3_w[f], taps, 16);
+  }
+  if (!choose_reciprocal(hp.l3_factor, &sp.l3_r)) return NET_ERR_RANGE;
+  for (int k = 0; k < F2; k++) {
+    std::memcpy(sp.l4_w[k], &hp.l4_weight[(size_t)k * F2], 16);
+    sp.l4_thr[k] = -(hp.l4_offset[k] >> 3);
+    sp.l4_off[k] = hp.l4_offset[k];
+    if (!choose_reciprocal(hp.l4_factor[k], &sp.l4_r[k])) return NET_ERR_RANGE;
+  }
+  const int T64 = d.T64(), T64A = d.T64_ALIGN();
+  if ((F2 * T64 + 3) / 4 > ND5_MAX) return NET_ERR_UNSUPPORTED;
+  for (int n = 0; n < N_OUT; n++) {
+    int8_t* dst = (int8_t*)sp.l5_w[n];
+    for (int k = 0; k < F2; k++)
+      for (int v = 0; v < T64; v++) dst[k * T64 + v] = hp.l5_weight[(size_t)n * F2 * T64A + k * T64A + v];
+    sp.l5_b[n] = hp.l5_bias[n];
+  }
+  if (!choose_reciprocal(hp.l5_factor, &sp.l5_r)) return NET_ERR_RANGE;
+  return NET_OK;
+}
+
+// ---- compiled configurations --------------------------------------------------------------
+using CfgB = Cfg<22, 1125>;  // BCI-IV-2a: 22 channels x 1125 samples (configs A, B, D, E)
+using CfgC = Cfg<64, 1000>;  // high-density variant: 64 channels x 1000 samples (config C)
+
+template <class K>
+struct Launch {
+  static int blocks_per_cu(int device) {
+    (void)device;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_forward<K>, NTHREADS, 0) != hipSuccess || nb < 1)
+      nb = 1;
+    return nb;
+  }
+};
+
+enum class Variant { None, B22x1125, C64x1000 };
+
+Variant variant_of(const Dims& d) {
+  if (d.C == 22 && d.T == 1125) return Variant::B22x1125;
+  if (d.C == 64 && d.T == 1000) return Variant::C64x1000;
+  return Variant::None;
+}
+
+size_t trial_stride(const Dims& d) { return ((size_t)d.C * d.T + 15) / 16 * 16; }
+
+// ---- global state --------------------------------------------------------------------------
+struct DeviceState {
+  std::mutex mu;
+  uint64_t gen = 0;           // params generation uploaded
+  DevParams* d_params = nullptr;
+  int8_t* d_in = nullptr;     // single-trial scratch
+  int8_t* d_out = nullptr;
+  size_t scratch = 0;
+  int cus = 0;
+  int blocks_per_cu = 0;
+};
+
+std::mutex g_mu;
+std::shared_ptr<const HostParams> g_host;
+std::shared_ptr<const DevParams> g_dev;
+uint64_t g_gen = 0;
+DeviceState g_devs[MAX_DEVICES];
+int g_single_device = 0;
+thread_local int t_last_error = NET_OK;
+
+inline int hip_err(hipError_t e) { return e == hipSuccess ? NET_OK : NET_ERR_HIP - (int)e; }
+
+struct DeviceGuard {  // restores the caller's current device
+  int old = -1;
+  explicit DeviceGuard(int dev) { if (hipGetDevice(&old) != hipSuccess) old = -1; (void)hipSetDevice(dev); }
+  ~DeviceGuard() { if (old >= 0) (void)hipSetDevice(old); }
+};
+
+struct Snapshot {
+  std::shared_ptr<const HostParams> host;
+  std::shared_ptr<const DevParams> dev;
+  uint64_t gen;
+};
+
+Snapshot snapshot() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return Snapshot{g_host, g_dev, g_gen};
+}
+
+// Ensure `dev` holds the current parameters; called with ds.mu held and the device current.
+int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
+  if (!s.host) return NET_ERR_NO_PARAMS;
+  if (ds.cus == 0) {
+    int cus = 0;
+    hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return hip_err(e);
+    ds.cus = cus;
+  }
+  if (!ds.d_params) {
+    hipError_t e = hipMalloc((void**)&ds.d_params, sizeof(DevParams));
+    if (e != hipSuccess) return hip_err(e);
+  }
+  if (ds.gen != s.gen) {
+    hipError_t e = hipMemcpy(ds.d_params, s.dev.get(), sizeof(DevParams), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_err(e);
+    ds.gen = s.gen;
+  }
+  return NET_OK;
+}
+
+int ensure_scratch(DeviceState& ds, size_t bytes) {
+  if (ds.scratch >= bytes) return NET_OK;
+  if (ds.d_in) (void)hipFree(ds.d_in);
+  if (ds.d_out) (void)hipFree(ds.d_out);
+  ds.d_in = ds.d_out = nullptr;
+  ds.scratch = 0;
+  hipError_t e = hipMalloc((void**)&ds.d_in, bytes);
+  if (e != hipSuccess) return hip_err(e);
+  e = hipMalloc((void**)&ds.d_out, bytes);
+  if (e != hipSuccess) return hip_err(e);
+  ds.scratch = bytes;
+  return NET_OK;
+}
+
+template <class K>
+int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y, size_t B,
+                     hipStream_t st, int32_t* info) {
+  if (ds.blocks_per_cu == 0) ds.blocks_per_cu = Launch<K>::blocks_per_cu(0);
+  const size_t cap = (size_t)ds.cus * (size_t)ds.blocks_per_cu;
+  const int grid = (int)(B < cap ? B : cap);
+  if (info) { info[0] = grid; info[1] = NTHREADS; info[2] = K::LDS; return NET_OK; }
+  if (B == 0) return NET_OK;
+  hipLaunchKernelGGL(k_forward<K>, dim3(grid), dim3(NTHREADS), 0, st, p, x, y, (int)B);
+  return hip_err(hipGetLastError());
+}
+
+int launch_forward(Variant v, DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y,
+                   size_t B, hipStream_t st, int32_t* info = nullptr) {
+  switch (v) {
+    case Variant::B22x1125: return launch_forward_t<CfgB>(ds, p, x, y, B, st, info);
+    case Variant::C64x1000: return launch_forward_t<CfgC>(ds, p, x, y, B, st, info);
+    default: return NET_ERR_UNSUPPORTED;
+  }
+}
+
+int launch_layer(Variant v, const DevParams* p, const int8_t* in, int8_t* out, int stage) {
+  switch (v) {
+    case Variant::B22x1125:
+      hipLaunchKernelGGL(k_layer<CfgB>, dim3(1), dim3(NTHREADS), 0, 0, p, in, out, stage);
+      break;
+    case Variant::C64x1000:
+      hipLaunchKernelGGL(k_layer<CfgC>, dim3(1), dim3(NTHREADS), 0, 0, p, in, out, stage);
+      break;
+    default: return NET_ERR_UNSUPPORTED;
+  }
+  return hip_err(hipGetLastError());
+}
+
+// Runs one reference-layout single-trial stage on the single-trial device.
+// stage 0 = whole model (input [T][C_ALIGN]); 1..5 = net_layerN; 6 = flip.
+int run_single(int stage, const int8_t* in, int8_t* out) {
+  if (!in || !out) return NET_ERR_INVALID;
+  Snapshot s = snapshot();
+  if (!s.host) return NET_ERR_NO_PARAMS;
+  const Dims& d = s.host->d;
+  const Variant v = variant_of(d);
+  if (v == Variant::None) return NET_ERR_UNSUPPORTED;
+  const int dev = g_single_device;
+  DeviceState& ds = g_devs[dev];
+  std::lock_guard<std::mutex> lk(ds.mu);
+  DeviceGuard guard(dev);
+  int rc = ensure_device(ds, dev, s);
+  if (rc) return rc;
+  const size_t xs = trial_stride(d);
+  size_t in_bytes, out_bytes;
+  std::vector<int8_t> hin;
+  switch (stage) {
+    case 0:
+    case 1: {  // reference input [T][C_ALIGN] -> packed [T][C]
+      hin.assign(xs, 0);
+      for (int t = 0; t < d.T; t++) std::memcpy(&hin[(size_t)t * d.C], in + (size_t)t * d.C_ALIGN(), d.C);
+      in_bytes = xs;
+      out_bytes = stage == 0 ? (size_t)d.N : (size_t)d.F1 * d.T_ALIGN();
+      break;
+    }
+    case 2: in_bytes = (size_t)d.F1 * d.T_ALIGN(); out_bytes = (size_t)d.F2 * d.T8_ALIGN(); break;
+    case 3: in_bytes = out_bytes = (size_t)d.F2 * d.T8_ALIGN(); break;
+    case 4: in_bytes = (size_t)d.T8() * d.F2; out_bytes = (size_t)d.F2 * d.T64_ALIGN(); break;
+    case 5: in_bytes = (size_t)d.F2 * d.T64_ALIGN(); out_bytes = (size_t)d.N; break;
+    case 6: in_bytes = out_bytes = (size_t)d.F2 * d.T8_ALIGN(); break;
+    default: return NET_ERR_INVALID;
+  }
+  rc = ensure_scratch(ds, xs > (size_t)d.F1 * d.T_ALIGN() ? xs + 64 : (size_t)d.F1 * d.T_ALIGN() + 64);
+  if (rc) return rc;
+  hipError_t e = hipMemcpy(ds.d_in, hin.empty() ? (const void*)in : (const void*)hin.data(), in_bytes,
+                           hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_err(e);
+  if (stage == 0)
+    rc = launch_forward(v, ds, ds.d_params, ds.d_in, ds.d_out, 1, 0);
+  else
+    rc = launch_layer(v, ds.d_params, ds.d_in, ds.d_out, stage);
+  if (rc) return rc;
+  e = hipMemcpy(out, ds.d_out, out_bytes, hipMemcpyDeviceToHost);
+  return hip_err(e);
+}
+
+}  // namespace
+
+// ================================ C ABI ======================================================
+extern "C" {
+
+int net_version(void) { return MIBMINET_VERSION; }
+
+const char* net_error_string(int code) {
+  switch (code) {
+    case NET_OK: return "ok";
+    case NET_ERR_INVALID: return "invalid argument";
+    case NET_ERR_NO_PARAMS: return "no parameters loaded";
+    case NET_ERR_UNSUPPORTED: return "unsupported network configuration";
+    case NET_ERR_BLOB: return "malformed parameter blob";
+    case NET_ERR_RANGE: return "parameters outside the exact requantisation envelope";
+    default:
+      if (code <= NET_ERR_HIP) return hipGetErrorString((hipError_t)(NET_ERR_HIP - code));
+      return "unknown error";
+  }
+}
+
+int net_params_load(const void* blob, size_t len) {
+  auto hp = std::make_shared<HostParams>();
+  int rc = parse_blob(blob, len, *hp);
+  if (rc) return rc;
+  if (variant_of(hp->d) == Variant::None) return NET_ERR_UNSUPPORTED;
+  auto dp = std::make_shared<DevParams>();
+  rc = build_devparams(*hp, *dp);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_host = hp;
+  g_dev = dp;
+  g_gen++;
+  return NET_OK;
+}
+
+void net_params_unload(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_host.reset();
+  g_dev.reset();
+  g_gen++;
+}
+
+int net_params_dims(int32_t* dims) {
+  if (!dims) return NET_ERR_INVALID;
+  Snapshot s = snapshot();
+  if (!s.host) {
+    for (int i = 0; i < 7; i++) dims[i] = 0;
+    return NET_ERR_NO_PARAMS;
+  }
+  const Dims& d = s.host->d;
+  dims[0] = d.C; dims[1] = d.T; dims[2] = d.F1; dims[3] = d.F2; dims[4] = d.N; dims[5] = d.wbits; dims[6] = 1;
+  return NET_OK;
+}
+
+size_t net_trial_stride(void) {
+  Snapshot s = snapshot();
+  return s.host ? trial_stride(s.host->d) : 0;
+}
+
+int net_set_device(int device) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) return hip_err(e);
+  if (device < 0 || device >= n || device >= MAX_DEVICES) return NET_ERR_INVALID;
+  g_single_device = device;
+  return NET_OK;
+}
+
+int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream) {
+  if ((!x || !y) && B) return NET_ERR_INVALID;
+  if (((uintptr_t)x & 15) != 0) return NET_ERR_INVALID;
+  if (device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
+  Snapshot s = snapshot();
+  if (!s.host) return NET_ERR_NO_PARAMS;
+  const Variant v = variant_of(s.host->d);
+  if (v == Variant::None) return NET_ERR_UNSUPPORTED;
+  DeviceState& ds = g_devs[device];
+  std::lock_guard<std::mutex> lk(ds.mu);
+  DeviceGuard guard(device);
+  int rc = ensure_device(ds, device, s);
+  if (rc) return rc;
+  return launch_forward(v, ds, ds.d_params, x, y, B, (hipStream_t)stream);
+}
+
+int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device) {
+  int rc = net_model_compute_batch_async(x, y, B, device, nullptr);
+  if (rc) return rc;
+  DeviceGuard guard(device);
+  return hip_err(hipStreamSynchronize(nullptr));
+}
+
+int net_launch_info(size_t B, int device, int32_t* out) {
+  if (!out || device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
+  Snapshot s = snapshot();
+  if (!s.host) return NET_ERR_NO_PARAMS;
+  const Variant v = variant_of(s.host->d);
+  DeviceState& ds = g_devs[device];
+  std::lock_guard<std::mutex> lk(ds.mu);
+  DeviceGuard guard(device);
+  int rc = ensure_device(ds, device, s);
+  if (rc) return rc;
+  return launch_forward(v, ds, nullptr, nullptr, nullptr, B, nullptr, out);
+}
+
+int net_forward(const int8_t* p_data, int8_t* p_output) { return run_single(0, p_data, p_output); }
+
+void net_model_compute(const int8_t* p_data, int8_t* p_output) { t_last_error = run_single(0, p_data, p_output); }
+void net_layer1(const int8_t* p_data, int8_t* p_result) { t_last_error = run_single(1, p_data, p_result); }
+void net_layer2(const int8_t* p_data, int8_t* p_result) { t_last_error = run_single(2, p_data, p_result); }
+void net_layer3(const int8_t* p_data, int8_t* p_result) { t_last_error = run_single(3, p_data, p_result); }
+void net_layer3_flip_inplace(int8_t* p_data) { t_last_error = run_single(6, p_data, p_data); }
+void net_layer4(const int8_t* p_data, int8_t* p_result) { t_last_error = run_single(4, p_data, p_result); }
+void net_layer5(const int8_t* p_data, int8_t* p_result) { t_last_error = run_single(5, p_data, p_result); }
+
+int net_last_error(void) { return t_last_error; }
+
+}  // extern "C"

@@ -1,0 +1,241 @@
+"""ctypes binding of libmibminet.so (include/mibminet.h) — the Python mirror of the reference's
+C model/layer API (edge-eegnet_wolf/src/cl/net/model.h, layers.h).
+
+There is no CPU fallback: if the library cannot be loaded, or a call fails, a ``NetError`` is
+raised.  Single-trial functions take host NumPy arrays in the reference layouts; the batched
+function takes device pointers (e.g. ``torch.Tensor.data_ptr()`` of CUDA/HIP tensors).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+from .params import ParamSet
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmibminet.so")
+
+NET_OK = 0
+NET_ERR_INVALID = -1
+NET_ERR_NO_PARAMS = -2
+NET_ERR_UNSUPPORTED = -3
+NET_ERR_BLOB = -4
+NET_ERR_RANGE = -5
+NET_ERR_HIP = -100
+
+EXPORTED_SYMBOLS = (
+    "net_model_compute", "net_forward", "net_layer1", "net_layer2", "net_layer3",
+    "net_layer3_flip_inplace", "net_layer4", "net_layer5", "net_last_error", "net_params_load",
+    "net_params_dims", "net_params_unload", "net_trial_stride", "net_model_compute_batch",
+    "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
+    "net_version",
+)
+
+
+class NetError(RuntimeError):
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        msg = _lib_error_string(code)
+        super().__init__(f"{what}: {msg} (code {code})" if what else f"{msg} (code {code})")
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def _lib_error_string(code: int) -> str:
+    try:
+        return load().net_error_string(code).decode()
+    except Exception:  # pragma: no cover - library missing
+        return "error"
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libmibminet.so (raises OSError — loudly — if it is missing or fails to load)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"libmibminet.so not found at {path}: build it with `make -C mi-bminet_amd`"
+                      " (there is no CPU fallback)")
+    L = ctypes.CDLL(path)
+    vp, sz, i, i8p = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p
+    for name in ("net_model_compute", "net_layer1", "net_layer2", "net_layer3", "net_layer4", "net_layer5"):
+        getattr(L, name).argtypes = [i8p, i8p]
+        getattr(L, name).restype = None
+    L.net_forward.argtypes = [i8p, i8p]
+    L.net_forward.restype = i
+    L.net_layer3_flip_inplace.argtypes = [i8p]
+    L.net_layer3_flip_inplace.restype = None
+    L.net_last_error.argtypes = []
+    L.net_last_error.restype = i
+    L.net_params_load.argtypes = [vp, sz]
+    L.net_params_load.restype = i
+    L.net_params_dims.argtypes = [vp]
+    L.net_params_dims.restype = i
+    L.net_params_unload.argtypes = []
+    L.net_params_unload.restype = None
+    L.net_trial_stride.argtypes = []
+    L.net_trial_stride.restype = sz
+    L.net_model_compute_batch.argtypes = [vp, vp, sz, i]
+    L.net_model_compute_batch.restype = i
+    L.net_model_compute_batch_async.argtypes = [vp, vp, sz, i, vp]
+    L.net_model_compute_batch_async.restype = i
+    L.net_set_device.argtypes = [i]
+    L.net_set_device.restype = i
+    L.net_launch_info.argtypes = [sz, i, vp]
+    L.net_launch_info.restype = i
+    L.net_error_string.argtypes = [i]
+    L.net_error_string.restype = ctypes.c_char_p
+    L.net_version.argtypes = []
+    L.net_version.restype = i
+    _lib = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != NET_OK:
+        raise NetError(rc, what)
+
+
+# ---- parameters -------------------------------------------------------------------------------
+_loaded: Optional[ParamSet] = None
+
+
+def params_load(ps: ParamSet) -> None:
+    """net_params_load(blob) — replaces the generated net.h globals of the reference."""
+    global _loaded
+    blob = ps.to_blob()
+    buf = ctypes.create_string_buffer(blob, len(blob))
+    _check(load().net_params_load(buf, len(blob)), "net_params_load")
+    _loaded = ps
+
+
+def params_load_blob(blob: bytes) -> None:
+    global _loaded
+    buf = ctypes.create_string_buffer(blob, len(blob))
+    _check(load().net_params_load(buf, len(blob)), "net_params_load")
+    _loaded = ParamSet.from_blob(blob)
+
+
+def params_dims() -> dict:
+    arr = (ctypes.c_int32 * 7)()
+    rc = load().net_params_dims(arr)
+    if rc == NET_ERR_NO_PARAMS:
+        return {}
+    _check(rc, "net_params_dims")
+    return dict(zip(("C", "T", "F1", "F2", "N", "weight_bits", "loaded"), list(arr)))
+
+
+def params_unload() -> None:
+    global _loaded
+    load().net_params_unload()
+    _loaded = None
+
+
+def trial_stride() -> int:
+    return int(load().net_trial_stride())
+
+
+def _dims():
+    if _loaded is None:
+        raise NetError(NET_ERR_NO_PARAMS, "no parameters loaded")
+    return _loaded.dims
+
+
+# ---- reference single-trial API (host arrays, reference layouts) --------------------------------
+def _call_void(name: str, x: np.ndarray, out: np.ndarray) -> np.ndarray:
+    L = load()
+    getattr(L, name)(x.ctypes.data, out.ctypes.data)
+    _check(L.net_last_error(), name)
+    return out
+
+
+def net_model_compute(x_tc_align: np.ndarray) -> np.ndarray:
+    """model.h:40 — x: [T][C_ALIGN] int8 -> logits [N] int8."""
+    d = _dims()
+    x = np.ascontiguousarray(x_tc_align, np.int8).reshape(d.T, d.C_ALIGN)
+    return _call_void("net_model_compute", x, np.empty(d.N, np.int8))
+
+
+def net_layer1(x_tc_align: np.ndarray) -> np.ndarray:
+    d = _dims()
+    x = np.ascontiguousarray(x_tc_align, np.int8).reshape(d.T, d.C_ALIGN)
+    return _call_void("net_layer1", x, np.empty((d.F1, d.T_ALIGN), np.int8))
+
+
+def net_layer2(y1: np.ndarray) -> np.ndarray:
+    d = _dims()
+    x = np.ascontiguousarray(y1, np.int8).reshape(d.F1, d.T_ALIGN)
+    return _call_void("net_layer2", x, np.empty((d.F2, d.T8_ALIGN), np.int8))
+
+
+def net_layer3(y2: np.ndarray) -> np.ndarray:
+    d = _dims()
+    x = np.ascontiguousarray(y2, np.int8).reshape(d.F2, d.T8_ALIGN)
+    return _call_void("net_layer3", x, np.empty((d.F2, d.T8_ALIGN), np.int8))
+
+
+def net_layer3_flip_inplace(y3: np.ndarray) -> np.ndarray:
+    """layers.h:107 — [F2][T8_ALIGN] -> [T8][F2] (in place on a copy; returned)."""
+    d = _dims()
+    buf = np.ascontiguousarray(y3, np.int8).reshape(d.F2 * d.T8_ALIGN).copy()
+    L = load()
+    L.net_layer3_flip_inplace(buf.ctypes.data)
+    _check(L.net_last_error(), "net_layer3_flip_inplace")
+    return buf
+
+
+def net_layer4(y3t: np.ndarray) -> np.ndarray:
+    d = _dims()
+    x = np.zeros(d.F2 * d.T8_ALIGN, np.int8)
+    src = np.ascontiguousarray(y3t, np.int8).ravel()
+    x[: min(src.size, x.size)] = src[: x.size]
+    return _call_void("net_layer4", x, np.empty((d.F2, d.T64_ALIGN), np.int8))
+
+
+def net_layer5(y4: np.ndarray) -> np.ndarray:
+    d = _dims()
+    x = np.ascontiguousarray(y4, np.int8).reshape(d.F2, d.T64_ALIGN)
+    return _call_void("net_layer5", x, np.empty(d.N, np.int8))
+
+
+def set_device(device: int) -> None:
+    _check(load().net_set_device(device), "net_set_device")
+
+
+# ---- batched device API -----------------------------------------------------------------------
+def model_compute_batch(x_ptr: int, y_ptr: int, B: int, device: int = 0, stream: Optional[int] = None) -> None:
+    """net_model_compute_batch(_async): x_ptr/y_ptr are device pointers ([B][trial_stride] int8
+    and [B][N] int8).  With ``stream`` the launch is enqueued without a host sync."""
+    L = load()
+    if stream is None:
+        _check(L.net_model_compute_batch(x_ptr, y_ptr, B, device), "net_model_compute_batch")
+    else:
+        _check(L.net_model_compute_batch_async(x_ptr, y_ptr, B, device, stream), "net_model_compute_batch_async")
+
+
+def launch_info(B: int, device: int = 0) -> dict:
+    arr = (ctypes.c_int32 * 3)()
+    _check(load().net_launch_info(B, device, arr), "net_launch_info")
+    return {"grid": arr[0], "threads": arr[1], "lds_bytes": arr[2]}
+
+
+def forward_torch(x, params: Optional[ParamSet] = None, stream=None):
+    """Convenience: x is a CUDA/HIP int8 torch tensor [B][trial_stride] -> logits [B][N] tensor."""
+    import torch
+
+    if params is not None:
+        params_load(params)
+    d = _dims()
+    if x.dtype != torch.int8 or not x.is_cuda or not x.is_contiguous():
+        raise ValueError("x must be a contiguous int8 device tensor [B][trial_stride]")
+    B = x.shape[0]
+    if x.numel() != B * trial_stride():
+        raise ValueError(f"x must be [B][{trial_stride()}]")
+    y = torch.empty((B, d.N), dtype=torch.int8, device=x.device)
+    s = torch.cuda.current_stream(x.device) if stream is None else stream
+    model_compute_batch(x.data_ptr(), y.data_ptr(), B, x.device.index or 0, s.cuda_stream)
+    return y

@@ -1,0 +1,84 @@
+"""The C-ABI library loads without a GPU, exports every symbol include/mibminet.h declares and
+validates parameters on the host.  No compute calls are made here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from mibminet import lib
+from mibminet.params import ParamSet
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    text = open(os.path.join(ROOT, "include", "mibminet.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(net_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_symbols_exported():
+    L = lib.load()
+    names = declared_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(lib.EXPORTED_SYMBOLS)
+
+
+def test_version_and_errors():
+    L = lib.load()
+    assert L.net_version() == 1
+    assert L.net_error_string(0) == b"ok"
+    assert b"blob" in L.net_error_string(lib.NET_ERR_BLOB)
+
+
+@pytest.mark.parametrize("C,T,wbits", [(22, 1125, 8), (64, 1000, 8), (22, 1125, 4)])
+def test_params_load_host(C, T, wbits):
+    ps = ParamSet.synthetic(seed=9, C=C, T=T, weight_bits=wbits)
+    lib.params_load(ps)
+    d = lib.params_dims()
+    assert (d["C"], d["T"], d["F1"], d["F2"], d["N"], d["weight_bits"], d["loaded"]) == (C, T, 16, 16, 4, wbits, 1)
+    assert lib.trial_stride() == (C * T + 15) // 16 * 16
+    lib.params_unload()
+    assert lib.params_dims() == {}
+    assert lib.trial_stride() == 0
+
+
+def test_params_load_rejects():
+    L = lib.load()
+    bad = b"x" * 100
+    assert L.net_params_load(bad, len(bad)) == lib.NET_ERR_BLOB
+    ps = ParamSet.synthetic(seed=1)
+    blob = ps.to_blob()
+    assert L.net_params_load(blob[:-4], len(blob) - 4) == lib.NET_ERR_BLOB
+    # an unsupported geometry (no compiled kernel) fails loudly
+    ps2 = ParamSet.synthetic(seed=1, C=8, T=512)
+    b2 = ps2.to_blob()
+    assert L.net_params_load(b2, len(b2)) == lib.NET_ERR_UNSUPPORTED
+    # offsets beyond the exact float envelope
+    ps3 = ParamSet.synthetic(seed=1)
+    ps3.l1_offset[0] = 4_000_000
+    b3 = ps3.to_blob()
+    assert L.net_params_load(b3, len(b3)) == lib.NET_ERR_RANGE
+
+
+def test_no_params_errors():
+    lib.params_unload()
+    L = lib.load()
+    x = np.zeros((1125, 24), np.int8)
+    y = np.zeros(4, np.int8)
+    assert L.net_forward(x.ctypes.data, y.ctypes.data) == lib.NET_ERR_NO_PARAMS
+    L.net_model_compute(x.ctypes.data, y.ctypes.data)
+    assert L.net_last_error() == lib.NET_ERR_NO_PARAMS
+    assert L.net_model_compute_batch(None, None, 0, 0) == lib.NET_ERR_NO_PARAMS
+
+
+def test_appendix_b_factors_accepted():
+    """The real-looking (Appendix B) factors pass the exact-reciprocal verification."""
+    from mibminet.params import appendix_b_net
+    net, cfg, _ = appendix_b_net(0)
+    lib.params_load(ParamSet.from_quantlab(net, cfg))
+    lib.params_unload()
