@@ -78,15 +78,24 @@ bool verify_reciprocal(int32_t fac, float r) {
   return true;
 }
 
-bool choose_reciprocal(int32_t fac, float* out) {
+bool choose_reciprocal(int32_t fac, float* out, float* magic_c = nullptr) {
+  // magic_c != nullptr: additionally require c = -(1.5 * 2^23) * r to be exact in f32, so that
+  // fma(bits_as_float(v + 0x4B400000), r, c) == RN(v * r) (layer 1's one-instruction requant).
   if (fac == 0) return false;
   const double F = std::fabs((double)fac);
   const double target = (1.0 / F) * (1.0 + std::ldexp(1.0, -22));
   float r = (float)target;
   if ((double)r < target) r = std::nextafterf(r, INFINITY);
-  for (int tries = 0; tries < 256; tries++) {
+  for (int tries = 0; tries < 4096; tries++) {
     const float rs = fac < 0 ? -r : r;
-    if (verify_reciprocal(fac, rs)) { *out = rs; return true; }
+    bool ok = true;
+    if (magic_c) {
+      const double cd = -12582912.0 * (double)rs;
+      const float cf = (float)cd;
+      ok = ((double)cf == cd);
+      if (ok) *magic_c = cf;
+    }
+    if (ok && verify_reciprocal(fac, rs)) { *out = rs; return true; }
     r = std::nextafterf(r, INFINITY);
   }
   return false;
@@ -200,7 +209,7 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     for (int j = 0; j < 16; j++) {
       const int f = P == 2 ? 8 * t + (j >> 1) : j;
       dp.l1_cinit[t][j] = hp.l1_offset[f] + FMAGIC_I;
-      if (!choose_reciprocal(hp.l1_factor[f], &dp.l1_r[t][j])) return NET_ERR_RANGE;
+      if (!choose_reciprocal(hp.l1_factor[f], &dp.l1_r[t][j], &dp.l1_c[t][j])) return NET_ERR_RANGE;
     }
   }
   // layer 2: A operand = banded weights; row i <-> shift n(i) so that lane (c, h) register r
@@ -212,7 +221,9 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
         int8_t bytes[16];
         for (int jj = 0; jj < 16; jj++) {
-          const int kp = 32 * s + 16 * hh + jj;  // position in the 96-byte row window
+          const int kq = 32 * s + 16 * hh + jj;  // K-slot
+          // position in the 96-byte row window (P == 2: parity-split K order, see l2_boff)
+          const int kp = P == 2 ? (kq < 48 ? 2 * kq : 2 * (kq - 48) + 1) : kq;
           const int idx = kp - n - 1;            // tap (torch order)
           bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
         }
@@ -230,8 +241,15 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     std::memcpy(sp.l3_w[f], taps, 16);
   }
   if (!choose_reciprocal(hp.l3_factor, &sp.l3_r)) return NET_ERR_RANGE;
+  // layer 4: B operand of MFMA 32x32x32 = W4^T; lane (column k, half h): k-slots 16h..16h+15
+  // hold input channels f = 16h + jj (only h == 0 is populated, F2 == 16), columns k >= 16 zero
+  for (int lane = 0; lane < 64; lane++) {
+    const int k = lane & 31, hh = lane >> 5;
+    int8_t bytes[16] = {0};
+    if (k < F2 && hh == 0) std::memcpy(bytes, &hp.l4_weight[(size_t)k * F2], 16);
+    std::memcpy(&dp.sp.l4_bfrag[lane], bytes, 16);
+  }
   for (int k = 0; k < F2; k++) {
-    std::memcpy(sp.l4_w[k], &hp.l4_weight[(size_t)k * F2], 16);
     sp.l4_thr[k] = -(hp.l4_offset[k] >> 3);
     sp.l4_off[k] = hp.l4_offset[k];
     if (!choose_reciprocal(hp.l4_factor[k], &sp.l4_r[k])) return NET_ERR_RANGE;
@@ -500,7 +518,7 @@ int net_set_device(int device) {
 
 int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream) {
   if ((!x || !y) && B) return NET_ERR_INVALID;
-  if (((uintptr_t)x & 15) != 0) return NET_ERR_INVALID;
+  if (((uintptr_t)x & 15) != 0 || ((uintptr_t)y & 3) != 0) return NET_ERR_INVALID;
   if (device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
