@@ -1,0 +1,73 @@
+"""Static batch split: shard bounds, and a world_size-2 gloo run on CPU whose
+per-rank shards (computed by the oracle in place of the GPU) concatenate to the whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from mibminet.params import ParamSet, pack_trials
+from mibminet.shard import shard_bounds
+
+
+@pytest.mark.parametrize("batch,world", [(0, 2), (1, 2), (7, 2), (65536, 8), (524288, 8), (13, 5)])
+def test_shard_bounds_partition(batch, world):
+    spans = [shard_bounds(batch, world, r) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == batch
+    for (a, b), (c, d) in zip(spans, spans[1:]):
+        assert b == c
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_bounds_rejects():
+    with pytest.raises(ValueError):
+        shard_bounds(10, 0, 0)
+    with pytest.raises(ValueError):
+        shard_bounds(10, 2, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, blob, x, out_dir):
+    import sys
+
+    import torch.distributed as dist
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import oracle
+    from mibminet.params import ParamSet
+    from mibminet.shard import forward_shard, gather_logits
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ps = ParamSet.from_blob(blob)
+    co = oracle.COracle(ps)
+    y = forward_shard(x, rank, world, compute=lambda part: co.batch(part, nthreads=1))
+    full = gather_logits(y, x.shape[0], world)
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"), full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("batch", [9, 16])
+def test_gloo_world2_static_split(tmp_path, batch):
+    import oracle
+
+    ps = ParamSet.synthetic(seed=5, C=8, T=512)
+    rng = np.random.default_rng(batch)
+    x = pack_trials(rng.integers(-60, 60, size=(batch, 8, 512)))
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), ps.to_blob(), x, str(tmp_path)), nprocs=world, join=True)
+    want = oracle.COracle(ps).batch(x, nthreads=2)
+    for r in range(world):
+        got = np.load(tmp_path / f"rank{r}.npy")
+        assert np.array_equal(got, want)

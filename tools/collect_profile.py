@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Turns a tools/profile_round.sh output directory into the committed profile artefacts:
+
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_pmc.csv            per-dispatch FETCH_SIZE / WRITE_SIZE of the forward kernel
+  profiles/pmc_traffic.json         HBM bytes per launch (read by bench.py for roofline.traffic)
+  profiles/<tag>_bench_*.json       the bench JSON lines
+
+FETCH_SIZE is doubled (gfx950 tallies 128-B fabric reads at 64 B: MI355X_MICROARCH.md, HBM
+section); WRITE_SIZE is taken as is.  Both counters report kB (1024 B).
+
+    python tools/collect_profile.py gpurun_out/prof_r01 r01
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "k_forward"
+
+
+def one(pattern):
+    hits = sorted(glob.glob(pattern, recursive=True))
+    if not hits:
+        raise SystemExit(f"missing {pattern}")
+    return hits[0]
+
+
+def pmc_values(path, counter):
+    vals = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(one(f"{src}/trace/**/*kernel_stats.csv"), f"{prof}/{tag}_kernel_stats.csv")
+    for cfg in ("b22", "c64", "d22"):
+        p = f"{src}/bench_{cfg}.json"
+        if os.path.exists(p):
+            lines = [l for l in open(p) if l.startswith("{")]
+            if lines:
+                open(f"{prof}/{tag}_bench_{cfg}.json", "w").write(lines[-1])
+    fetch = pmc_values(one(f"{src}/pmc_fetch/**/*counter_collection.csv"), "FETCH_SIZE")
+    write = pmc_values(one(f"{src}/pmc_write/**/*counter_collection.csv"), "WRITE_SIZE")
+    with open(f"{prof}/{tag}_pmc.csv", "w") as f:
+        f.write("dispatch,FETCH_SIZE_kB,WRITE_SIZE_kB\n")
+        for i in range(max(len(fetch), len(write))):
+            fv = fetch[i] if i < len(fetch) else ""
+            wv = write[i] if i < len(write) else ""
+            f.write(f"{i},{fv},{wv}\n")
+    # skip the first (warm-up) dispatch
+    fk = sorted(fetch[1:] or fetch)[len(fetch[1:] or fetch) // 2]
+    wk = sorted(write[1:] or write)[len(write[1:] or write) // 2]
+    read_bytes = 2 * fk * 1024
+    write_bytes = wk * 1024
+    tj = {"config": "b22", "batch": 65536, "kernel": "k_forward<Cfg<22,1125>>",
+          "fetch_size_kB_raw": fk, "write_size_kB": wk,
+          "read_bytes_corrected": read_bytes, "write_bytes": write_bytes,
+          "hbm_bytes_per_launch": read_bytes + write_bytes,
+          "alg_bytes_per_launch": (22 * 1125 + 4) * 65536,
+          "source": f"profiles/{tag}_pmc.csv (median over dispatches after the first; FETCH_SIZE x2 per gfx950 correction)"}
+    json.dump(tj, open(f"{prof}/pmc_traffic.json", "w"), indent=1)
+    print(json.dumps(tj, indent=1))
+    print(open(f"{prof}/{tag}_kernel_stats.csv").read())
+
+
+if __name__ == "__main__":
+    main()
