@@ -1,0 +1,113 @@
+// forward_common.hpp — types, parameter images and helpers of the gfx950 forward kernel
+// (forward_wg.hpp).
+//
+// Requantisation y = clip(trunc((acc + off) / fac), -128, 127) is computed as
+// clip(int(float(acc + off) * r)) with r chosen on the host (mibminet.hip: choose_reciprocal) and
+// verified at every step boundary of the clipped output range, so it is bit-exact to C's integer
+// division for every reachable accumulator.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mib {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr int F2 = 16;          // filters (F1 == F2, D == 1)
+constexpr int N_OUT = 4;        // classes
+constexpr int L2_TAPS = 64;
+constexpr int L3_TAPS = 16;
+constexpr int ND5_MAX = 96;     // dwords of the flattened layer-4 output (F2*T64 <= 384)
+constexpr int FMAGIC_I = 0x4B400000;   // bit pattern of 1.5 * 2^23
+
+// Diagnostic phase stamps (tools/probe.hip builds with -DMIB_STAMPS; compiled out otherwise).
+#ifdef MIB_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define MIB_STAMP_INIT unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  unsigned long long _st_t = __builtin_amdgcn_s_memtime(); \
+  const unsigned long long _st_t0 = _st_t, _st_r0 = __builtin_amdgcn_s_memrealtime();
+#define MIB_STAMP(i) { const unsigned long long _t = __builtin_amdgcn_s_memtime(); _st_acc[i] += _t - _st_t; _st_t = _t; }
+#define MIB_STAMP_FLUSH(cond) if (cond) { for (int _i = 0; _i < 6; _i++) atomicAdd(&g_stamps[_i], _st_acc[_i]); \
+  atomicAdd(&g_stamps[6], __builtin_amdgcn_s_memtime() - _st_t0); atomicAdd(&g_stamps[7], __builtin_amdgcn_s_memrealtime() - _st_r0); \
+  atomicAdd(&g_stamps[8], 1ull); }
+#else
+#define MIB_STAMP_INIT
+#define MIB_STAMP(i)
+#define MIB_STAMP_FLUSH(cond)
+#endif
+
+__host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+__host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }
+// smallest multiple of 4 >= x whose dword count is odd (conflict-free strided dword reads)
+__host__ __device__ constexpr int odd_dwords(int x) { return ((x + 3) / 4 % 2) ? (x + 3) / 4 * 4 : (x + 3) / 4 * 4 + 4; }
+
+// Parameters read into LDS by every workgroup.
+struct SmallParams {
+  v4i l4_bfrag[64];       // layer-4 B operand per lane (block diagonal, see host)
+  int l2_thr[F2];         // -(net_l2_offset >> 3)
+  int l2_off[F2];
+  float l2_r[F2];
+  int l4_thr[F2];
+  int l4_off[F2];
+  float l4_r[F2];
+  int l5_w[N_OUT][ND5_MAX];  // flattened [k][v] order, zero padded
+  int l5_b[N_OUT];
+  float l3_r;
+  float l5_r;
+  int pad[2];
+};
+
+// Operand fragments and requantisation constants, built by the host from the net.h arrays.
+struct DevParams {
+  v4i l1_wfrag[2][64];      // layer-1 B operand per N-tile and lane
+  int l1_cinit[2][16];      // offset + FMAGIC_I per N-tile column
+  float l1_r[2][16];        // reciprocal per N-tile column
+  float l1_c[2][16];        // -(1.5 * 2^23) * r, exact
+  v4i l2_afrag[F2][3][64];  // layer-2 A operand (banded weights) per filter, K-step and lane
+  int l2_thr[F2];
+  int l2_off[F2];
+  float l2_r[F2];
+  long l3_afrag[F2][64];    // layer-3 A operand (16 shifts x 32-byte band) per filter and lane
+  SmallParams sp;
+};
+
+__device__ __forceinline__ int rq(int v, float r) {
+  const int t = (int)((float)v * r);
+  return min(max(t, -128), 127);
+}
+
+// int32 -> saturated int8 pairs (gfx950 v_ashr_pk_i8_i32, shift 0): a to byte 0, b to byte 1.
+// The op_sel form writes bytes 2/3 and keeps bytes 0/1 (checked on hardware by
+// tools/isa_probe.hip).
+__device__ __forceinline__ unsigned sat8x2(int a, int b) {
+  unsigned r;
+  asm("v_ashr_pk_i8_i32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ unsigned sat8x4(int a, int b, int c, int d) {
+  unsigned r = sat8x2(a, b);
+  asm("v_ashr_pk_i8_i32 %0, %1, %2, 0 op_sel:[0,0,0,1]" : "+v"(r) : "v"(c), "v"(d));
+  return r;
+}
+
+// Layer-1 per-lane constants of one N-tile (kept as a scalarisable struct: arrays of these
+// fields get merged into vector loads of a stack slot by LLVM and end up in scratch).
+struct L1Tile {
+  v4i wf;
+  int ci;
+  float rr, cc;
+};
+
+// sum_{i<8} max(acc[base + i], thr) + off  (the REORDER_BN ReLU + sum-pool of layers 2 and 4)
+template <int BASE>
+__device__ __forceinline__ int pool8(const v16i& acc, int thr, int off) {
+  int m[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = max(acc[BASE + i], thr);
+  return ((m[0] + m[1] + m[2]) + (m[3] + m[4]) + (m[5] + m[6])) + (m[7] + off);
+}
+
+}  // namespace mib

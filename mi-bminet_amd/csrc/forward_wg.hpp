@@ -1,0 +1,518 @@
+// forward_wg.hpp — gfx950 fused forward kernel of the int8 MI-BMInet (edgeEEGNet) network.
+//
+// One workgroup of NWAVES = 8 wave64s owns one trial at a time and walks a grid-strided list of
+// trials (persistent; two workgroups per CU, i.e. four waves per SIMD, so one workgroup's
+// barriers are covered by the other's work).  Per trial:
+//   layer1  spatial C->16 contraction on MFMA i32_16x16x64_i8.  A = 16 time groups x 64-byte
+//           input window (P = 2 samples of C <= 32 channels per group, or 1 sample of up to 64)
+//           read straight from HBM into registers (4-byte-aligned 16-B loads, prefetched one
+//           trial ahead while the current trial runs layers 2-5); B = per-(filter, parity)
+//           weight fragment; C-init = offset + float magic, so requant is one exact packed fma,
+//           a truncating convert and a saturating pack (v_ashr_pk_i8_i32) per 2-4 samples.
+//                                                    (reference: layer1.c:53-101)
+//   layer2  64-tap depthwise temporal xcorr as a banded-Toeplitz GEMM on MFMA i32_32x32x32_i8:
+//           A = 32 output shifts x 96-tap band of the filter (held in registers; rows permuted so
+//           that each lane owns two whole pool-8 windows), B = 16-byte slices of the layer-1 row
+//           at immediate offsets.  32 column blocks per filter form its full tile; the TB
+//           remaining blocks of the wave's FPW filters share one tail tile (block-diagonal K:
+//           each filter's MFMAs read the zero row for the other filter's columns), so the
+//           ReLU / sum-pool 8 / requant VALU work is not spent on empty columns.
+//                                                    (reference: layer2.c:56-118, xcorr.c:44)
+//   layer3  16-tap depthwise conv on MFMA i32_16x16x32_i8: A = 16 shifts x 32-byte band of the
+//           filter (registers), B = aligned 8-byte slices of the layer-2 row (columns = blocks of
+//           16 outputs); written transposed [u][f] (the reference's flip is index math).
+//                                                    (reference: layer3.c:49-79, conv.c:105)
+//   layer4  16x16 pointwise on MFMA i32_32x32x32_i8 with a block-diagonal B (two 32-sample time
+//           blocks per MFMA, all 64 lanes busy) + ReLU + pool 8 + requant.
+//                                                    (reference: layer4.c:51-149)
+//   layer5  F2*T64 -> 4 linear + bias + requant: one wave, 16 lanes per class, DPP row
+//           reduction, one dword store.              (reference: layer5.c:43-89)
+#pragma once
+#include "forward_common.hpp"
+
+namespace mib {
+namespace wg {
+
+constexpr int NWAVES = 8;             // waves per workgroup (one trial per workgroup)
+constexpr int FPW = F2 / NWAVES;      // layer-2 / layer-3 filters per wave
+constexpr int NTHREADS = 64 * NWAVES;
+constexpr int WPE = 4;                // waves per SIMD (two workgroups per CU)
+constexpr int PF_MAX = 9;             // layer-1 blocks per wave prefetched one trial ahead
+static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wave");
+
+template <int C_, int T_>
+struct Cfg {
+  static constexpr int C = C_, T = T_;
+  static constexpr int P = (C <= 32) ? 2 : 1;          // samples per 64-byte L1 window
+  static constexpr int GS = P * C;                      // bytes per time group
+  static constexpr int NB1 = (T + 16 * P - 1) / (16 * P);  // L1 blocks of 16 groups
+  static constexpr int NBW = (NB1 + NWAVES - 1) / NWAVES;  // L1 blocks per wave (max)
+  static constexpr int PF = cmin(NBW, PF_MAX);          // of which prefetched a trial ahead
+  static constexpr int T8 = T / 8, T64 = T8 / 8;
+  static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
+  static constexpr int MT = NB2 / 32;                   // full L2 tiles per filter
+  static constexpr int TB = NB2 - 32 * MT;              // tail blocks per filter
+  // layer-1 rows hold positions pos = t + 32 (32 leading zeros = the xcorr pad of 31, aligned).
+  // P == 2: parity-split planes [pos & 1][pos >> 1]: each lane's 4 outputs (one parity) are
+  // contiguous and layer 2's K-window slices are 16-B aligned.
+  static constexpr int NPOS = cmax(32 + 16 * P * NB1, 32 * (NB2 - 1) + 96);
+  static constexpr int PLANE = align16((NPOS + P - 1) / P);
+  static constexpr int Y1ROW = P * PLANE;
+  static constexpr int XTRIAL = align16(T * C);         // batched trial stride (bytes)
+  static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
+  static constexpr int Y2ROW = odd_dwords(cmax(T8 + 24, 16 * NB3 + 24));
+  static constexpr int NT4 = (8 * T64 + 63) / 64;       // L4 MFMAs of 64 time samples
+  static constexpr int Y3ROWS = cmax(64 * NT4, T8);
+  // y3t rows are 20 bytes apart (16 filters + 4 pad): layer 3's 2-byte stores from 64 lanes
+  // (64 different rows) then hit 64 different banks; layer 4 reads a row with one unaligned
+  // ds_read_b128 (3 per trial)
+  static constexpr int Y3S = 20;
+  static constexpr int ND5 = (F2 * T64 + 3) / 4;        // layer-5 input dwords
+  static constexpr int N5L = (ND5 + 15) / 16;           // layer-5 dwords per lane
+  // LDS carve
+  static constexpr int OFF_Y1 = 0;
+  static constexpr int OFF_Y2 = OFF_Y1 + F2 * Y1ROW;
+  static constexpr int OFF_Y3 = OFF_Y2 + align16(F2 * Y2ROW) + 256;  // layer-3 reads may run 256 B past
+  static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S);
+  static constexpr int OFF_ZERO = OFF_Y4 + align16(64 * N5L);
+  static constexpr int OFF_SP = OFF_ZERO + 128;
+  static constexpr int LDS = align16(OFF_SP + (int)sizeof(SmallParams));
+  static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
+  static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
+  static_assert(T64 >= 1, "T >= 64");
+  static_assert(16 * N5L <= ND5_MAX, "layer-5 input too long");
+  static_assert(MT >= 1, "at least one full layer-2 tile");
+  static_assert(FPW * TB <= 32, "tail columns of a wave fit one tile");
+  static_assert(OFF_ZERO >= F2 * Y1ROW, "zero-row addressing stays non-negative");
+};
+
+// byte offset of layer-1 output (filter f, sample t) inside the LDS rows
+template <class K>
+__device__ __forceinline__ int y1_index(int f, int t) {
+  if constexpr (K::P == 2) return f * K::Y1ROW + (t & 1) * K::PLANE + ((t + 32) >> 1);
+  else return f * K::Y1ROW + 32 + t;
+}
+
+// layer-2 B operand: byte offset (within a filter's rows, column block 0) of the 16-byte slice of
+// lane half h, K-step s.  P == 2: half h reads parity plane h, plane bytes 16 s .. 16 s + 15 of the
+// block's window (K-slot 32 s + 16 h + j <-> position 2 (16 s + j) + h); P == 1: natural order.
+// The band fragments built on the host use the same K order.
+template <class K>
+__device__ __forceinline__ int l2_boff(int s, int h) {
+  if constexpr (K::P == 2) return h * K::PLANE + 16 * s;
+  else return 32 * s + 16 * h;
+}
+
+// Per-lane register state that lives across the trial loop.
+template <class K>
+struct Regs {
+  L1Tile t0, t1;
+  __device__ __forceinline__ const L1Tile& tile(int t) const { return t == 0 ? t0 : t1; }
+  __device__ __forceinline__ L1Tile& tile(int t) { return t == 0 ? t0 : t1; }
+  v4i af[FPW][3];          // layer-2 band fragments of the wave's filters
+  int thr2[FPW], off2[FPW];
+  float r2[FPW];
+  long a3[FPW];            // layer-3 band fragments of the wave's filters
+  v4i pf[K::PF];           // layer-1 fragments prefetched one trial ahead
+};
+
+// ---- layer-1 input ---------------------------------------------------------------------------
+// A fragment of block `blk` (16 time groups): lane (j, g) holds bytes
+// [ (16 blk + j) * GS + 16 g, +16 ) of the trial.  Unconditional, branch-free loads (a branch
+// around a load makes the compiler drain vmcnt at the join); blocks past the end are clamped to
+// the last block, windows running past the trial are clamped to its last 16 bytes and shifted
+// back into place by fix_a().
+template <class K>
+__device__ __forceinline__ int a_offset(int blk, int lane) {
+  return (blk * 16 + (lane & 15)) * K::GS + 16 * (lane >> 4);
+}
+
+template <class K>
+__device__ __forceinline__ v4i load_a(const int8_t* __restrict__ xt, int blk, int lane) {
+  const int b = blk < K::NB1 ? blk : K::NB1 - 1;
+  const int off = min(a_offset<K>(b, lane), K::XTRIAL - 16);
+  return __builtin_nontemporal_load((const v4i*)(xt + off));
+}
+
+template <class K>
+__device__ __forceinline__ v4i fix_a(v4i v, int blk, int lane) {
+  if (blk != K::NB1 - 1) return v;  // wave-uniform; only the last block can run past the trial
+  const int k = (a_offset<K>(blk, lane) - (K::XTRIAL - 16)) >> 2;  // dwords to shift down
+  if (k <= 0) return v;
+  v4i r;
+  r.x = k == 1 ? v.y : k == 2 ? v.z : k == 3 ? v.w : 0;
+  r.y = k == 1 ? v.z : k == 2 ? v.w : 0;
+  r.z = k == 1 ? v.w : 0;
+  r.w = 0;
+  return r;
+}
+
+template <class K>
+__device__ __forceinline__ void prefetch_l1(const int8_t* __restrict__ xt, Regs<K>& R, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < K::PF; i++) R.pf[i] = load_a<K>(xt, wave + NWAVES * i, lane);
+}
+
+template <class K>
+__device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t* smem, Regs<K>& R,
+                                      int tid, int wave, int lane) {
+#pragma unroll
+  for (int t = 0; t < K::P; t++) {
+    L1Tile& T = R.tile(t);
+    T.wf = prm->l1_wfrag[t][lane];
+    T.ci = prm->l1_cinit[t][lane & 15];
+    T.rr = prm->l1_r[t][lane & 15];
+    T.cc = prm->l1_c[t][lane & 15];
+  }
+#pragma unroll
+  for (int fi = 0; fi < FPW; fi++) {
+    const int f = wave * FPW + fi;
+#pragma unroll
+    for (int s = 0; s < 3; s++) R.af[fi][s] = prm->l2_afrag[f][s][lane];
+    R.thr2[fi] = prm->l2_thr[f];
+    R.off2[fi] = prm->l2_off[f];
+    R.r2[fi] = prm->l2_r[f];
+    R.a3[fi] = prm->l3_afrag[f][lane];
+  }
+  // small parameters -> LDS
+  const v4i* src = (const v4i*)&prm->sp;
+  v4i* dst = (v4i*)(smem + K::OFF_SP);
+  for (int i = tid; i < (int)(sizeof(SmallParams) / 16); i += NTHREADS) dst[i] = src[i];
+  // everything else zero: layer-1 pads (positions [0,32) and past the last block), layer-2 pads
+  // ([0,8) and [8+T8, Y2ROW)) and the zero row are never rewritten
+  v4i* z = (v4i*)smem;
+  for (int i = tid; i < K::OFF_SP / 16; i += NTHREADS) z[i] = (v4i){0, 0, 0, 0};
+}
+
+// ---- layer 1 ---------------------------------------------------------------------------------
+// One layer-1 block: 16 time groups x 16 filters (P == 2: two N-tiles of 8 filters x 2 parities).
+// MAYBE_LAST: the block may be the trial's last one (samples >= T are masked to zero).
+template <class K, bool MAYBE_LAST>
+__device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const Regs<K>& R, int lane) {
+  const int j = lane & 15, g = lane >> 4;
+  v4i accs[K::P];
+#pragma unroll
+  for (int t = 0; t < K::P; t++) {  // both N-tiles' MFMAs before either requant
+    const L1Tile& T = R.tile(t);
+    accs[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, T.wf, (v4i){T.ci, T.ci, T.ci, T.ci}, 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < K::P; t++) {
+    const L1Tile& T = R.tile(t);
+    const v4i acc = accs[t];
+    // acc bits = 1.5*2^23 + (dot + off) as f32; fma(x, r, -1.5*2^23*r) == RN((dot+off)*r)
+    const f2 rr2 = {T.rr, T.rr}, cc2 = {T.cc, T.cc};
+    const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(acc[0]), __int_as_float(acc[1])}, rr2, cc2);
+    const f2 q23 = __builtin_elementwise_fma((f2){__int_as_float(acc[2]), __int_as_float(acc[3])}, rr2, cc2);
+    int y[4] = {(int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]};  // trunc toward zero
+    // lane column j = (filter 8t + j/2, parity j&1) when P == 2, filter j when P == 1;
+    // row 4g + r = time group 16 blk + 4g + r
+    const int p = (K::P == 2) ? (j & 1) : 0;
+    const int f = (K::P == 2) ? 8 * t + (j >> 1) : j;
+    if constexpr (MAYBE_LAST) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) y[r] = (K::P * (16 * blk + 4 * g + r) + p < K::T) ? y[r] : 0;
+    }
+    const int t0 = K::P * (16 * blk + 4 * g) + p;  // first of the lane's 4 samples (stride P)
+    *(unsigned*)(smem_y1 + y1_index<K>(f, t0)) = sat8x4(y[0], y[1], y[2], y[3]);
+  }
+}
+
+// Layer 1: x[T][C] (HBM, via R.pf) -> y1 rows (LDS, position 32 + t).  Prefetches the next
+// trial's fragments (xnext) into R.pf once the current ones are consumed.
+template <class K>
+__device__ __forceinline__ void layer1(const int8_t* __restrict__ xt, const int8_t* __restrict__ xnext,
+                                       int8_t* smem_y1, Regs<K>& R, int wave, int lane) {
+  constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
+  v4i xa[NX > 0 ? NX : 1];
+#pragma unroll
+  for (int i = 0; i < NX; i++) xa[i] = load_a<K>(xt, wave + NWAVES * (K::PF + i), lane);
+  // rounds in which every wave has a block and none is the trial's last block
+  constexpr int NSAFE = (K::NB1 - 1) / NWAVES;
+#pragma unroll
+  for (int i = 0; i < NSAFE; i++) {
+    const v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
+    l1_block<K, false>(a, wave + NWAVES * i, smem_y1, R, lane);
+  }
+#pragma unroll
+  for (int i = NSAFE; i < K::NBW; i++) {
+    const int blk = wave + NWAVES * i;
+    if (blk < K::NB1) {
+      v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
+      a = fix_a<K>(a, blk, lane);
+      l1_block<K, true>(a, blk, smem_y1, R, lane);
+    }
+  }
+  prefetch_l1<K>(xnext, R, wave, lane);
+}
+
+// ---- layer 2 ---------------------------------------------------------------------------------
+// Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].
+__device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, float r) {
+  const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r, r};
+  return sat8x2((int)q[0], (int)q[1]);
+}
+
+// Layer 2: y1 rows -> y2 rows (LDS, position 8 + u).  Full tiles of the wave's filters, then the
+// shared tail tile (filter fi's blocks 32 MT + b -> column TB fi + b).
+template <class K>
+__device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, const int8_t* zero,
+                                       const SmallParams* sp, const Regs<K>& R, int wave, int lane) {
+  const int c = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int mt = 0; mt < K::MT; mt++)
+#pragma unroll
+    for (int fi = 0; fi < FPW; fi++) {
+      const int f = wave * FPW + fi;
+      const int8_t* pb = smem_y1 + f * K::Y1ROW + (32 / K::P) * (32 * mt + c);
+      v16i acc = {};
+#pragma unroll
+      for (int s = 0; s < 3; s++)
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, h)), acc, 0, 0, 0);
+      // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
+      const unsigned w = l2_out(acc, R.thr2[fi], R.off2[fi], R.r2[fi]);
+      const int u0 = 4 * (32 * mt + c) + 2 * h;
+      int8_t* dst = smem_y2 + f * K::Y2ROW + 8 + u0;
+      if (128 * (mt + 1) <= K::T8 || u0 + 1 < K::T8) *(unsigned short*)dst = (unsigned short)w;
+      else if (u0 < K::T8) *dst = (int8_t)w;
+    }
+  if constexpr (K::TB > 0) {
+    const int fi_c = c / K::TB, b = c % K::TB;  // this lane's tail column: filter slot, block
+    v16i tacc = {};
+#pragma unroll
+    for (int fi = 0; fi < FPW; fi++) {
+      const int f = wave * FPW + fi;
+      const int8_t* pb = (fi_c == fi) ? smem_y1 + f * K::Y1ROW + (32 / K::P) * (32 * K::MT + b)
+                                      : zero + 48 * h - l2_boff<K>(0, h);  // reads zeros
+#pragma unroll
+      for (int s = 0; s < 3; s++)
+        tacc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, h)), tacc, 0, 0, 0);
+    }
+    const bool valid = fi_c < FPW;
+    const int fc = wave * FPW + (valid ? fi_c : 0);
+    const unsigned w = l2_out(tacc, sp->l2_thr[fc], sp->l2_off[fc], sp->l2_r[fc]);
+    const int u0 = 4 * (32 * K::MT + b) + 2 * h;
+    if (valid && u0 < K::T8) {
+      int8_t* dst = smem_y2 + fc * K::Y2ROW + 8 + u0;
+      if (u0 + 1 < K::T8) *(unsigned short*)dst = (unsigned short)w;
+      else *dst = (int8_t)w;
+    }
+  }
+}
+
+// ---- layer 3 ---------------------------------------------------------------------------------
+// Per filter one MFMA i32_16x16x32_i8: A row r = 16-tap band shifted by r (host-built, a3),
+// B column = block of 16 outputs: 32 bytes of the layer-2 row from byte 16 col (output u uses row
+// bytes u+1 .. u+16: pad 7, stored at +8); lane (col, g) loads its aligned 8 bytes.  D lane
+// (col, g) holds outputs 16 col + 4g .. +3 of each of the wave's two filters; the two filters'
+// bytes of one output are adjacent in y3t[u][f] and go out as one 2-byte store.
+template <class K>
+__device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, const SmallParams* sp,
+                                       const Regs<K>& R, int wave, int lane) {
+  const int col = lane & 15, g = lane >> 4;
+  const float r3 = sp->l3_r;
+  unsigned w[FPW];
+#pragma unroll
+  for (int fi = 0; fi < FPW; fi++) {
+    const int f = wave * FPW + fi;
+    const long bv = *(const long*)(smem_y2 + f * K::Y2ROW + 16 * col + 8 * g);
+    v4i acc = {0, 0, 0, 0};
+    acc = __builtin_amdgcn_mfma_i32_16x16x32_i8(R.a3[fi], bv, acc, 0, 0, 0);
+    const f2 q01 = (f2){(float)acc[0], (float)acc[1]} * (f2){r3, r3};
+    const f2 q23 = (f2){(float)acc[2], (float)acc[3]} * (f2){r3, r3};
+    w[fi] = sat8x4((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
+  }
+  // interleave the two filters: pair i = bytes (f0[i], f1[i])
+  const unsigned p01 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u);  // f0[0] f1[0] f0[1] f1[1]
+  const unsigned p23 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u);  // f0[2] f1[2] f0[3] f1[3]
+  const int u = 16 * col + 4 * g;
+  int8_t* dst = smem_y3 + u * K::Y3S + FPW * wave;
+  if (u + 3 < K::T8) {
+    *(unsigned short*)dst = (unsigned short)p01;
+    *(unsigned short*)(dst + K::Y3S) = (unsigned short)(p01 >> 16);
+    *(unsigned short*)(dst + 2 * K::Y3S) = (unsigned short)p23;
+    *(unsigned short*)(dst + 3 * K::Y3S) = (unsigned short)(p23 >> 16);
+  } else {
+    if (u < K::T8) *(unsigned short*)dst = (unsigned short)p01;
+    if (u + 1 < K::T8) *(unsigned short*)(dst + K::Y3S) = (unsigned short)(p01 >> 16);
+    if (u + 2 < K::T8) *(unsigned short*)(dst + 2 * K::Y3S) = (unsigned short)p23;
+  }
+}
+
+// ---- layer 4 ---------------------------------------------------------------------------------
+// One wave.  MFMA t covers samples 64t .. 64t+63: A row i (lane (i, h)) = y3t[64t + 32h + n(i)] in
+// K-slots 16h..16h+15; B is block diagonal (columns c < 16: channel c on slots 0..15, columns
+// c >= 16: channel c-16 on slots 16..31), so column c of D = channel c & 15 of time block c >> 4.
+// Rows n(i) permuted so lane (c, h) register r = time 16h + r of that block: two pool-8 windows.
+template <class K>
+__device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, const SmallParams* sp, int lane) {
+  const int i = lane & 31, h = lane >> 5, k = i & 15;
+  const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
+  const v4i bw = sp->l4_bfrag[lane];
+  const int thr = sp->l4_thr[k], off = sp->l4_off[k];
+  const float r4 = sp->l4_r[k];
+  v4i a[K::NT4];
+#pragma unroll
+  for (int t = 0; t < K::NT4; t++) a[t] = *(const v4i*)(smem_y3 + (64 * t + 32 * h + n) * K::Y3S);  // unaligned (4 B)
+#pragma unroll
+  for (int t = 0; t < K::NT4; t++) {
+    v16i acc = {};
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[t], bw, acc, 0, 0, 0);
+    const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
+    const unsigned w = sat8x2((int)q[0], (int)q[1]);
+    const int v0 = 8 * t + 4 * (i >> 4) + 2 * h;
+    int8_t* dst = smem_y4 + k * K::T64 + v0;
+    if (v0 < K::T64) dst[0] = (int8_t)w;
+    if (v0 + 1 < K::T64) dst[1] = (int8_t)(w >> 8);
+  }
+}
+
+// ---- layer 5 ---------------------------------------------------------------------------------
+template <class K>
+__device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallParams* sp, int lane) {
+  const int n = lane >> 4, c = lane & 15;
+  int part = 0;
+#pragma unroll
+  for (int j = 0; j < K::N5L; j++) {
+    const int i = c + 16 * j;  // dwords past ND5 meet zero weights (l5_w is zero padded)
+    part = __builtin_amdgcn_sdot4(*(const int*)(smem_y4 + 4 * i), sp->l5_w[n][i], part, false);
+  }
+  // inclusive prefix sum within each 16-lane DPP row: lane 15 of the row holds the total
+  part += __builtin_amdgcn_update_dpp(0, part, 0x111, 0xF, 0xF, true);  // row_shr:1
+  part += __builtin_amdgcn_update_dpp(0, part, 0x112, 0xF, 0xF, true);  // row_shr:2
+  part += __builtin_amdgcn_update_dpp(0, part, 0x114, 0xF, 0xF, true);  // row_shr:4
+  part += __builtin_amdgcn_update_dpp(0, part, 0x118, 0xF, 0xF, true);  // row_shr:8
+  const int z = rq(part + sp->l5_b[n], sp->l5_r);
+  const unsigned z0 = (unsigned)__builtin_amdgcn_readlane(z, 15) & 255u;
+  const unsigned z1 = (unsigned)__builtin_amdgcn_readlane(z, 31) & 255u;
+  const unsigned z2 = (unsigned)__builtin_amdgcn_readlane(z, 47) & 255u;
+  const unsigned z3 = (unsigned)__builtin_amdgcn_readlane(z, 63);
+  return z0 | (z1 << 8) | (z2 << 16) | (z3 << 24);
+}
+
+// Fused forward over a batch (persistent, grid-strided over trials).
+template <class K>
+__global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_forward(
+    const DevParams* __restrict__ prm, const int8_t* __restrict__ x, int8_t* __restrict__ out, int B) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[K::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  Regs<K> R;
+  setup<K>(prm, smem, R, tid, wave, lane);
+  const SmallParams* sp = (const SmallParams*)(smem + K::OFF_SP);
+  if ((int)blockIdx.x < B) prefetch_l1<K>(x + (size_t)blockIdx.x * K::XTRIAL, R, wave, lane);
+  __syncthreads();
+  MIB_STAMP_INIT
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    const int bn = b + gridDim.x;
+    const int8_t* xt = x + (size_t)b * K::XTRIAL;
+    const int8_t* xn = bn < B ? x + (size_t)bn * K::XTRIAL : xt;  // last: harmless re-read
+    // laundered lane id: per-lane addresses of layers 2-5 are recomputed every trial instead of
+    // being hoisted out of the loop (they would be live across it and spill)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    MIB_STAMP(5)
+    layer1<K>(xt, xn, smem + K::OFF_Y1, R, wave, lane);
+    __syncthreads();
+    MIB_STAMP(0)
+    layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, smem + K::OFF_ZERO, sp, R, wave, ln);
+    __syncthreads();
+    MIB_STAMP(1)
+    layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, wave, ln);
+    __syncthreads();
+    MIB_STAMP(2)
+    // layers 4 and 5 on the last wave (no barrier: the next trial's layers 1-2 touch neither
+    // y3t nor y4, and the next layer 3 waits at two barriers this wave also passes)
+    if (wave == NWAVES - 1) {
+      layer4<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, ln);
+      MIB_STAMP(3)
+      const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, ln);
+      if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = z;
+    }
+    MIB_STAMP(4)
+  }
+  MIB_STAMP_FLUSH(tid == 64 * (NWAVES - 1))
+}
+
+// Single-trial, single-layer kernel for the reference's per-layer entry points (debug/parity):
+// reads the layer input in its reference layout, runs the same device code as k_forward and
+// writes the layer output in its reference layout (pads zero).
+template <class K>
+__global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict__ prm,
+                                                     const int8_t* __restrict__ in,
+                                                     int8_t* __restrict__ out, int stage) {
+  __shared__ __attribute__((aligned(16))) int8_t smem[K::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  Regs<K> R;
+  setup<K>(prm, smem, R, tid, wave, lane);
+  const SmallParams* sp = (const SmallParams*)(smem + K::OFF_SP);
+  constexpr int T_AL = (K::T + 3) & ~3, T8_AL = (K::T8 + 3) & ~3, T64_AL = (K::T64 + 3) & ~3;
+  int8_t* y1 = smem + K::OFF_Y1;
+  int8_t* y2 = smem + K::OFF_Y2;
+  int8_t* y3 = smem + K::OFF_Y3;
+  int8_t* y4 = smem + K::OFF_Y4;
+  __syncthreads();
+  if (stage == 1) {  // [T][C] packed (XTRIAL bytes) -> [F1][T_ALIGN]
+    prefetch_l1<K>(in, R, wave, lane);
+    layer1<K>(in, in, y1, R, wave, lane);
+    __syncthreads();
+    for (int i = tid; i < F2 * T_AL; i += NTHREADS) {
+      const int f = i / T_AL, t = i - f * T_AL;
+      out[i] = t < K::T ? y1[y1_index<K>(f, t)] : 0;
+    }
+  } else if (stage == 2) {  // [F1][T_ALIGN] -> [F2][T8_ALIGN]
+    for (int i = tid; i < F2 * K::T; i += NTHREADS) {
+      const int f = i / K::T, t = i - f * K::T;
+      y1[y1_index<K>(f, t)] = in[f * T_AL + t];
+    }
+    __syncthreads();
+    layer2<K>(y1, y2, smem + K::OFF_ZERO, sp, R, wave, lane);
+    __syncthreads();
+    for (int i = tid; i < F2 * T8_AL; i += NTHREADS) {
+      const int f = i / T8_AL, u = i - f * T8_AL;
+      out[i] = u < K::T8 ? y2[f * K::Y2ROW + 8 + u] : 0;
+    }
+  } else if (stage == 3) {  // [F2][T8_ALIGN] -> [F2][T8_ALIGN]
+    for (int i = tid; i < F2 * K::T8; i += NTHREADS) {
+      const int f = i / K::T8, u = i - f * K::T8;
+      y2[f * K::Y2ROW + 8 + u] = in[f * T8_AL + u];
+    }
+    __syncthreads();
+    layer3<K>(y2, y3, sp, R, wave, lane);
+    __syncthreads();
+    for (int i = tid; i < F2 * T8_AL; i += NTHREADS) {
+      const int f = i / T8_AL, u = i - f * T8_AL;
+      out[i] = u < K::T8 ? y3[u * K::Y3S + f] : 0;
+    }
+  } else if (stage == 4) {  // [T8][F2] -> [F2][T64_ALIGN]
+    for (int i = tid; i < K::Y3ROWS * F2; i += NTHREADS) y3[(i / F2) * K::Y3S + (i % F2)] = i < K::T8 * F2 ? in[i] : 0;
+    __syncthreads();
+    if (wave == 0) layer4<K>(y3, y4, sp, lane);
+    __syncthreads();
+    for (int i = tid; i < F2 * T64_AL; i += NTHREADS) {
+      const int k = i / T64_AL, v = i - k * T64_AL;
+      out[i] = v < K::T64 ? y4[k * K::T64 + v] : 0;
+    }
+  } else if (stage == 5) {  // [F2][T64_ALIGN] -> [N]
+    for (int i = tid; i < 64 * K::N5L; i += NTHREADS) {
+      const int k = i / K::T64, v = i - k * K::T64;
+      y4[i] = (k < F2) ? in[k * T64_AL + v] : 0;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const unsigned z = layer5<K>(y4, sp, lane);
+      if (lane == 0) *(unsigned*)out = z;
+    }
+  } else if (stage == 6) {  // flip [F2][T8_ALIGN] -> [T8][F2] (net_layer3_flip_inplace)
+    for (int i = tid; i < F2 * T8_AL; i += NTHREADS) y1[i] = in[i];
+    __syncthreads();
+    for (int i = tid; i < F2 * T8_AL; i += NTHREADS) {
+      const int u = i / F2, f = i - u * F2;
+      out[i] = u < K::T8 ? y1[f * T8_AL + u] : 0;
+    }
+  }
+}
+
+}  // namespace wg
+}  // namespace mib

@@ -4,7 +4,7 @@
 //   net.h arrays (edge-eegnet_wolf/data/gen_net_header.py:91-224),
 // * builds the gfx950 operand fragments and exact requantisation reciprocals (DevParams),
 // * uploads them lazily per device and dispatches the compiled (C, T) instantiations of the
-//   kernels in forward.hpp.
+//   kernel in forward_wg.hpp.
 // There is no CPU compute path: without a usable HIP device every entry point returns an error.
 #include <hip/hip_runtime.h>
 
@@ -18,7 +18,7 @@
 #include <vector>
 
 #include "../../include/mibminet.h"
-#include "forward.hpp"
+#include "forward_wg.hpp"
 
 using namespace mib;
 
@@ -222,8 +222,9 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         int8_t bytes[16];
         for (int jj = 0; jj < 16; jj++) {
           const int kq = 32 * s + 16 * hh + jj;  // K-slot
-          // position in the 96-byte row window (P == 2: parity-split K order, see l2_boff)
-          const int kp = P == 2 ? (kq < 48 ? 2 * kq : 2 * (kq - 48) + 1) : kq;
+          // position in the 96-byte row window.  P == 2: lane half hh reads
+          // parity plane hh, bytes 16s .. 16s+15 of the block's window; P == 1: natural order.
+          const int kp = P == 2 ? 2 * (16 * s + jj) + hh : kq;
           const int idx = kp - n - 1;            // tap (torch order)
           bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
         }
@@ -232,21 +233,38 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     dp.l2_thr[f] = -(hp.l2_offset[f] >> 3);
     dp.l2_off[f] = hp.l2_offset[f];
     if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f])) return NET_ERR_RANGE;
+    dp.sp.l2_thr[f] = dp.l2_thr[f];
+    dp.sp.l2_off[f] = dp.l2_off[f];
+    dp.sp.l2_r[f] = dp.l2_r[f];
+
   }
   SmallParams& sp = dp.sp;
-  // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed
+  // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed.
+  // A operand of MFMA i32_16x16x32_i8: row r (output shift within a block of 16), K-slot k (byte
+  // 16 col + k of the layer-2 row, which holds position k - 8 + 16 col): output u = 16 col + r
+  // uses bytes u+1 .. u+16, so A[r][k] = tap[k - r - 1].  Lane l holds row l & 15, K-slots
+  // 8 (l >> 4) .. +7.
   for (int f = 0; f < F2; f++) {
     int8_t taps[16];
     for (int j = 0; j < 16; j++) taps[j] = hp.l3_weight[(size_t)f * 16 + 15 - j];
-    std::memcpy(sp.l3_w[f], taps, 16);
+    for (int lane = 0; lane < 64; lane++) {
+      const int r = lane & 15, kg = lane >> 4;
+      int8_t bytes[8];
+      for (int jj = 0; jj < 8; jj++) {
+        const int j = 8 * kg + jj - r - 1;
+        bytes[jj] = (j >= 0 && j < 16) ? taps[j] : 0;
+      }
+      std::memcpy(&dp.l3_afrag[f][lane], bytes, 8);
+    }
   }
   if (!choose_reciprocal(hp.l3_factor, &sp.l3_r)) return NET_ERR_RANGE;
-  // layer 4: B operand of MFMA 32x32x32 = W4^T; lane (column k, half h): k-slots 16h..16h+15
-  // hold input channels f = 16h + jj (only h == 0 is populated, F2 == 16), columns k >= 16 zero
+  // layer 4: B operand of MFMA 32x32x32 = W4^T, block diagonal: lane (column k, half h) holds
+  // K-slots 16h..16h+15; columns 0..15 carry output channels 0..15 on slots 0..15 and columns
+  // 16..31 repeat them on slots 16..31 (a second 32-sample time block rides in the other K half).
   for (int lane = 0; lane < 64; lane++) {
     const int k = lane & 31, hh = lane >> 5;
     int8_t bytes[16] = {0};
-    if (k < F2 && hh == 0) std::memcpy(bytes, &hp.l4_weight[(size_t)k * F2], 16);
+    if ((k >> 4) == hh) std::memcpy(bytes, &hp.l4_weight[(size_t)(k & 15) * F2], 16);
     std::memcpy(&dp.sp.l4_bfrag[lane], bytes, 16);
   }
   for (int k = 0; k < F2; k++) {
@@ -267,19 +285,8 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
 }
 
 // ---- compiled configurations --------------------------------------------------------------
-using CfgB = Cfg<22, 1125>;  // BCI-IV-2a: 22 channels x 1125 samples (configs A, B, D, E)
-using CfgC = Cfg<64, 1000>;  // high-density variant: 64 channels x 1000 samples (config C)
-
-template <class K>
-struct Launch {
-  static int blocks_per_cu(int device) {
-    (void)device;
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_forward<K>, NTHREADS, 0) != hipSuccess || nb < 1)
-      nb = 1;
-    return nb;
-  }
-};
+using CfgB = wg::Cfg<22, 1125>;  // BCI-IV-2a: 22 channels x 1125 samples (configs A, B, D, E)
+using CfgC = wg::Cfg<64, 1000>;  // high-density variant: 64 channels x 1000 samples (config C)
 
 enum class Variant { None, B22x1125, C64x1000 };
 
@@ -365,15 +372,21 @@ int ensure_scratch(DeviceState& ds, size_t bytes) {
   return NET_OK;
 }
 
+// Persistent grid: as many resident workgroups as the occupancy allows (two per CU).
 template <class K>
 int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y, size_t B,
                      hipStream_t st, int32_t* info) {
-  if (ds.blocks_per_cu == 0) ds.blocks_per_cu = Launch<K>::blocks_per_cu(0);
+  if (ds.blocks_per_cu == 0) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wg::k_forward<K>, wg::NTHREADS, 0) != hipSuccess || nb < 1)
+      nb = 1;
+    ds.blocks_per_cu = nb;
+  }
   const size_t cap = (size_t)ds.cus * (size_t)ds.blocks_per_cu;
   const int grid = (int)(B < cap ? B : cap);
-  if (info) { info[0] = grid; info[1] = NTHREADS; info[2] = K::LDS; return NET_OK; }
+  if (info) { info[0] = grid; info[1] = wg::NTHREADS; info[2] = K::LDS; return NET_OK; }
   if (B == 0) return NET_OK;
-  hipLaunchKernelGGL(k_forward<K>, dim3(grid), dim3(NTHREADS), 0, st, p, x, y, (int)B);
+  hipLaunchKernelGGL(wg::k_forward<K>, dim3(grid), dim3(wg::NTHREADS), 0, st, p, x, y, (int)B);
   return hip_err(hipGetLastError());
 }
 
@@ -389,10 +402,10 @@ int launch_forward(Variant v, DeviceState& ds, const DevParams* p, const int8_t*
 int launch_layer(Variant v, const DevParams* p, const int8_t* in, int8_t* out, int stage) {
   switch (v) {
     case Variant::B22x1125:
-      hipLaunchKernelGGL(k_layer<CfgB>, dim3(1), dim3(NTHREADS), 0, 0, p, in, out, stage);
+      hipLaunchKernelGGL(wg::k_layer<CfgB>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
       break;
     case Variant::C64x1000:
-      hipLaunchKernelGGL(k_layer<CfgC>, dim3(1), dim3(NTHREADS), 0, 0, p, in, out, stage);
+      hipLaunchKernelGGL(wg::k_layer<CfgC>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
       break;
     default: return NET_ERR_UNSUPPORTED;
   }

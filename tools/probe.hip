@@ -1,5 +1,6 @@
 // Diagnostic probe (not part of the product): builds the library TU with -DMIB_STAMPS and
-// reports per-phase cycles of k_forward (s_memtime deltas of wave 0 of every workgroup).
+// reports per-phase cycles of the forward kernel (s_memtime deltas accumulated by the flushing
+// lane of every wave (one-wave kernel) or of one wave per workgroup (workgroup kernel)).
 // usage: probe <blob> [B] [iters]
 #include "../mi-bminet_amd/csrc/mibminet.hip"
 #include <chrono>
@@ -31,14 +32,14 @@ int main(int argc, char** argv) {
   unsigned long long st[16];
   hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
   int32_t info[3]; net_launch_info(B, 0, info);
-  const char* names[] = {"loop top", "layer1", "layer2", "layer3", "layer4", "layer5", "-", "-"};
+  const char* names[] = {"layer1", "layer2", "layer3", "layer4", "layer5+store", "loop top", "-", "-"};
   double trials = (double)B * iters;
   printf("B=%zu iters=%d  %.3f ms/launch  grid %d  lds %d\n", B, iters, ms / iters, info[0], info[2]);
   double tot = 0;
   for (int i = 0; i < 6; i++) tot += st[i];
   printf("  shader clock from s_memtime/s_memrealtime: %.3f GHz\n", 0.1 * (double)st[6] / (double)st[7]);
   for (int i = 0; i < 6; i++)
-    printf("  %-18s %8.0f cycles/trial/WG  (%4.1f%%)\n", names[i], st[i] / trials, 100.0 * st[i] / tot);
-  printf("  total %8.0f cycles per trial per WG (s_memtime ticks)\n", tot / trials);
+    printf("  %-18s %8.0f cycles/trial/flusher  (%4.1f%%)\n", names[i], st[i] / trials, 100.0 * st[i] / tot);
+  printf("  total %8.0f cycles per trial per flusher (s_memtime ticks), flushers %llu\n", tot / trials, st[8]);
   return 0;
 }
