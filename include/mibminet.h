@@ -95,6 +95,18 @@ int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device);
 /* Same, enqueued on `stream` (a hipStream_t of `device`, NULL = null stream), no host sync. */
 int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream);
 
+/* Input quantiser / transposer (the step before the path; reference
+ * edge-eegnet_wolf/data/gen_input_header.py:66-76 with python_utils/functional.py:308-334):
+ * x: DEVICE pointer to B float trials [B][C][T]; y: DEVICE pointer to the batched int8 layout
+ * ([B][stride], stride = C*T rounded up to 16, each trial [T][C], pad bytes zero), computed as
+ * trunc(clip(x / scale, -1, 1) * 127) in the input's precision.  scale = absMaxValue of the
+ * network's quant1 activation.  Enqueued on `stream` (NULL = null stream), no host sync.
+ * B <= 65535 per call. */
+int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, float scale, int device,
+                           void* stream);
+int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, double scale, int device,
+                           void* stream);
+
 /* Device used by the single-trial API (default 0). */
 int net_set_device(int device);
 

@@ -390,6 +390,19 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
   return z0 | (z1 << 8) | (z2 << 16) | (z3 << 24);
 }
 
+// Diagnostics only (tools/probe.hip builds): MIB_DIAG_NOBAR drops the in-loop barriers (wrong
+// results, timing insight), MIB_DIAG_SAME_TRIAL makes every trial read trial 0 (L2-resident).
+#ifdef MIB_DIAG_NOBAR
+#define MIB_LOOP_BARRIER() ((void)0)
+#else
+#define MIB_LOOP_BARRIER() __syncthreads()
+#endif
+#ifdef MIB_DIAG_SAME_TRIAL
+#define MIB_TRIAL_OFF(b) ((size_t)0 * (size_t)(b))
+#else
+#define MIB_TRIAL_OFF(b) ((size_t)(b) * K::XTRIAL)
+#endif
+
 // Fused forward over a batch (persistent, grid-strided over trials).
 template <class K>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_forward(
@@ -405,21 +418,21 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   MIB_STAMP_INIT
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const int bn = b + gridDim.x;
-    const int8_t* xt = x + (size_t)b * K::XTRIAL;
-    const int8_t* xn = bn < B ? x + (size_t)bn * K::XTRIAL : xt;  // last: harmless re-read
+    const int8_t* xt = x + MIB_TRIAL_OFF(b);
+    const int8_t* xn = bn < B ? x + MIB_TRIAL_OFF(bn) : xt;  // last: harmless re-read
     // laundered lane id: per-lane addresses of layers 2-5 are recomputed every trial instead of
     // being hoisted out of the loop (they would be live across it and spill)
     int ln = lane;
     asm volatile("" : "+v"(ln));
     MIB_STAMP(5)
     layer1<K>(xt, xn, smem + K::OFF_Y1, R, wave, lane);
-    __syncthreads();
+    MIB_LOOP_BARRIER();
     MIB_STAMP(0)
     layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, smem + K::OFF_ZERO, sp, R, wave, ln);
-    __syncthreads();
+    MIB_LOOP_BARRIER();
     MIB_STAMP(1)
     layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, wave, ln);
-    __syncthreads();
+    MIB_LOOP_BARRIER();
     MIB_STAMP(2)
     // layers 4 and 5 on the last wave (no barrier: the next trial's layers 1-2 touch neither
     // y3t nor y4, and the next layer 3 waits at two barriers this wave also passes)

@@ -19,6 +19,7 @@
 
 #include "../../include/mibminet.h"
 #include "forward_wg.hpp"
+#include "quantize.hpp"
 
 using namespace mib;
 
@@ -460,6 +461,19 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
   return hip_err(e);
 }
 
+template <class F>
+int quantize_input(const F* x, int8_t* y, size_t B, int C, int T, F scale, int device, void* stream) {
+  if ((!x || !y) && B) return NET_ERR_INVALID;
+  if (C < 1 || C > quant::CMAX || T < 1 || device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
+  if (B > 65535 || !(scale > 0)) return NET_ERR_INVALID;
+  if (B == 0) return NET_OK;
+  const int stride = (int)(((size_t)C * T + 15) / 16 * 16);
+  DeviceGuard guard(device);
+  dim3 grid((T + quant::TT - 1) / quant::TT, (unsigned)B);
+  hipLaunchKernelGGL(quant::k_quantize<F>, grid, dim3(quant::QTHREADS), 0, (hipStream_t)stream, x, y, C, T, stride, scale);
+  return hip_err(hipGetLastError());
+}
+
 }  // namespace
 
 // ================================ C ABI ======================================================
@@ -543,6 +557,14 @@ int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int devi
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
   return launch_forward(v, ds, ds.d_params, x, y, B, (hipStream_t)stream);
+}
+
+int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, float scale, int device, void* stream) {
+  return quantize_input<float>(x, y, B, C, T, scale, device, stream);
+}
+
+int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, double scale, int device, void* stream) {
+  return quantize_input<double>(x, y, B, C, T, scale, device, stream);
 }
 
 int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device) {

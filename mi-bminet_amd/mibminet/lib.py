@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "net_layer3_flip_inplace", "net_layer4", "net_layer5", "net_last_error", "net_params_load",
     "net_params_dims", "net_params_unload", "net_trial_stride", "net_model_compute_batch",
     "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
-    "net_version",
+    "net_version", "net_quantize_input_f32", "net_quantize_input_f64",
 )
 
 
@@ -91,6 +91,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_error_string.restype = ctypes.c_char_p
     L.net_version.argtypes = []
     L.net_version.restype = i
+    L.net_quantize_input_f32.argtypes = [vp, vp, sz, i, i, ctypes.c_float, i, vp]
+    L.net_quantize_input_f32.restype = i
+    L.net_quantize_input_f64.argtypes = [vp, vp, sz, i, i, ctypes.c_double, i, vp]
+    L.net_quantize_input_f64.restype = i
     _lib = L
     return L
 
@@ -238,4 +242,25 @@ def forward_torch(x, params: Optional[ParamSet] = None, stream=None):
     y = torch.empty((B, d.N), dtype=torch.int8, device=x.device)
     s = torch.cuda.current_stream(x.device) if stream is None else stream
     model_compute_batch(x.data_ptr(), y.data_ptr(), B, x.device.index or 0, s.cuda_stream)
+    return y
+
+
+def quantize_input_torch(x, scale: float, stream=None):
+    """Input quantiser (net_quantize_input_f32/_f64): x is a CUDA/HIP float32 or float64 tensor
+    [B][C][T] (the reference's input.npz layout); returns the batched int8 layout [B][stride]
+    (stride = C*T rounded up to 16, each trial [T][C]) that forward_torch consumes.  Semantics of
+    the reference's quantize_to_int (functional.py:308-334) in the input's precision."""
+    import torch
+
+    if not x.is_cuda or not x.is_contiguous() or x.dim() != 3 or x.dtype not in (torch.float32, torch.float64):
+        raise ValueError("x must be a contiguous float32/float64 device tensor [B][C][T]")
+    B, C, T = x.shape
+    stride = (C * T + 15) // 16 * 16
+    y = torch.empty((B, stride), dtype=torch.int8, device=x.device)
+    s = torch.cuda.current_stream(x.device) if stream is None else stream
+    fn = load().net_quantize_input_f32 if x.dtype == torch.float32 else load().net_quantize_input_f64
+    for lo in range(0, B, 65535):
+        n = min(65535, B - lo)
+        _check(fn(x[lo:].data_ptr(), y[lo:].data_ptr(), n, C, T, scale, x.device.index or 0, s.cuda_stream),
+               "net_quantize_input")
     return y

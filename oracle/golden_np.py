@@ -114,3 +114,28 @@ def forward(p, x: np.ndarray, return_all: bool = False):
     if return_all:
         return z, (y1, y2, y3, y4)
     return z
+
+
+def quantize_to_int(x: np.ndarray, scale_factor, num_levels: int = 255) -> np.ndarray:
+    """functional.py:308-334 (quantize_to_int) in the input's own precision: x / scale, clip to
+    [-1, 1], * (num_levels - 1) / 2 (evaluated left to right like the reference), truncated toward
+    zero.  ``scale_factor`` is taken in x's dtype (the reference's absMaxValue is a float32
+    scalar from net.npz, which NumPy keeps in float32 against a float32 array)."""
+    assert num_levels % 2
+    x = np.asarray(x)
+    s = x.dtype.type(scale_factor)
+    y = x / s
+    y = np.clip(y, x.dtype.type(-1), x.dtype.type(1))
+    y = y * x.dtype.type(num_levels - 1) / x.dtype.type(2)
+    return np.trunc(y).astype(np.int64)
+
+
+def quantize_input(x: np.ndarray, scale_factor) -> np.ndarray:
+    """gen_input_header.py:66-76: quantize_to_int then transpose [B][C][T] -> [B][T][C], packed
+    into the batched layout of the GPU path (trial stride = C*T rounded up to 16, pad zero)."""
+    q = quantize_to_int(x, scale_factor)
+    B, C, T = q.shape
+    stride = (C * T + 15) // 16 * 16
+    out = np.zeros((B, stride), dtype=np.int8)
+    out[:, : C * T] = np.transpose(q, (0, 2, 1)).reshape(B, C * T).astype(np.int8)
+    return out
