@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--config", default="b22", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline wall time")
+    ap.add_argument("--cpu-seconds", type=float, default=25.0, help="target CPU-baseline wall time")
     ap.add_argument("--pcie", action="store_true",
                     help="also time the host-buffer path (pinned H2D + forward + D2H); reported as "
                          "'pcie_inclusive', never as value")

@@ -69,6 +69,25 @@ def main():
           "alg_bytes_per_launch": (22 * 1125 + 4) * 65536,
           "source": f"profiles/{tag}_pmc.csv (median over dispatches after the first; FETCH_SIZE x2 per gfx950 correction)"}
     json.dump(tj, open(f"{prof}/pmc_traffic.json", "w"), indent=1)
+    # agreement check: rocprofv3 kernel-trace durations of the timed dispatches vs the HIP-event
+    # average bench.py measured in the same (profiled) process
+    trace = one(f"{src}/trace/**/*kernel_trace.csv")
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            for r in csv.DictReader(open(trace)) if KERNEL in r["Kernel_Name"]]
+    prof_line = [l for l in open(f"{src}/trace.log") if l.startswith("{")][-1]
+    pb = json.loads(prof_line)
+    steps, warm = pb["steps"], pb["warmup"]
+    timed = durs[warm:warm + steps]
+    summary = {
+        "kernel": tj["kernel"],
+        "rocprof_dispatches": len(durs),
+        "rocprof_avg_ms_timed_dispatches": sum(timed) / len(timed),
+        "bench_hip_event_avg_ms_same_process": pb["roofline"]["avg_kernel_ms"],
+        "rel_diff": sum(timed) / len(timed) / pb["roofline"]["avg_kernel_ms"] - 1.0,
+        "note": "trace run = python3 bench.py --steps %d --warmup %d under rocprofv3 --kernel-trace --stats" % (steps, warm),
+    }
+    json.dump(summary, open(f"{prof}/{tag}_trace_vs_bench.json", "w"), indent=1)
+    print(json.dumps(summary, indent=1))
     print(json.dumps(tj, indent=1))
     print(open(f"{prof}/{tag}_kernel_stats.csv").read())
 
