@@ -46,7 +46,14 @@ struct Cfg {
   static constexpr int P = (C <= 32) ? 2 : 1;          // samples per 64-byte L1 window
   static constexpr int GS = P * C;                      // bytes per time group
   static constexpr int NB1 = (T + 16 * P - 1) / (16 * P);  // L1 blocks of 16 groups
-  static constexpr int NBW = (NB1 + NWAVES - 1) / NWAVES;  // L1 blocks per wave (max)
+  // layer-1 block split.  SPLIT: waves 0..NWAVES-2 take NBM blocks each (round robin) and the
+  // last wave, which also runs layers 4-5 at the end of the trial, takes the NL leftover
+  // blocks.  Otherwise plain round robin over all waves.
+  static constexpr bool SPLIT = NB1 % (NWAVES - 1) != 0 && NB1 % (NWAVES - 1) < NB1 / NWAVES;
+  static constexpr int NLW = SPLIT ? NWAVES - 1 : NWAVES;
+  static constexpr int NL = SPLIT ? NB1 % NLW : 0;
+  static constexpr int NBM = SPLIT ? (NB1 - NL) / NLW : (NB1 + NWAVES - 1) / NWAVES;
+  static constexpr int NBW = cmax(NBM, NL);             // L1 blocks per wave (max)
   static constexpr int PF = cmin(NBW, PF_MAX);          // of which prefetched a trial ahead
   static constexpr int T8 = T / 8, T64 = T8 / 8;
   static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
@@ -147,10 +154,25 @@ __device__ __forceinline__ v4i fix_a(v4i v, int blk, int lane) {
   return r;
 }
 
+// i-th layer-1 block of a wave (the last wave's unused slots repeat its last block: the loads
+// stay unconditional, the compute is skipped)
+template <class K>
+__device__ __forceinline__ int l1_blk(int wave, int i) {
+  if (!K::SPLIT) return min(wave + NWAVES * i, K::NB1 - 1);
+  if (wave < K::NLW) return wave + K::NLW * i;
+  return K::NB1 - K::NL + min(i, K::NL - 1);
+}
+
+template <class K>
+__device__ __forceinline__ int l1_count(int wave) {
+  if (!K::SPLIT) return (K::NB1 - wave + NWAVES - 1) / NWAVES;
+  return wave < K::NLW ? K::NBM : K::NL;
+}
+
 template <class K>
 __device__ __forceinline__ void prefetch_l1(const int8_t* __restrict__ xt, Regs<K>& R, int wave, int lane) {
 #pragma unroll
-  for (int i = 0; i < K::PF; i++) R.pf[i] = load_a<K>(xt, wave + NWAVES * i, lane);
+  for (int i = 0; i < K::PF; i++) R.pf[i] = load_a<K>(xt, l1_blk<K>(wave, i), lane);
 }
 
 template <class K>
@@ -226,21 +248,19 @@ __device__ __forceinline__ void layer1(const int8_t* __restrict__ xt, const int8
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
   v4i xa[NX > 0 ? NX : 1];
 #pragma unroll
-  for (int i = 0; i < NX; i++) xa[i] = load_a<K>(xt, wave + NWAVES * (K::PF + i), lane);
-  // rounds in which every wave has a block and none is the trial's last block
-  constexpr int NSAFE = (K::NB1 - 1) / NWAVES;
+  for (int i = 0; i < NX; i++) xa[i] = load_a<K>(xt, l1_blk<K>(wave, K::PF + i), lane);
+  const int n = l1_count<K>(wave);
 #pragma unroll
-  for (int i = 0; i < NSAFE; i++) {
-    const v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
-    l1_block<K, false>(a, wave + NWAVES * i, smem_y1, R, lane);
-  }
-#pragma unroll
-  for (int i = NSAFE; i < K::NBW; i++) {
-    const int blk = wave + NWAVES * i;
-    if (blk < K::NB1) {
+  for (int i = 0; i < K::NBW; i++) {
+    if (i < n) {  // wave-uniform
+      const int blk = l1_blk<K>(wave, i);
       v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
-      a = fix_a<K>(a, blk, lane);
-      l1_block<K, true>(a, blk, smem_y1, R, lane);
+      if (blk == K::NB1 - 1) {  // the trial's last block: windows past the end, samples >= T
+        a = fix_a<K>(a, blk, lane);
+        l1_block<K, true>(a, blk, smem_y1, R, lane);
+      } else {
+        l1_block<K, false>(a, blk, smem_y1, R, lane);
+      }
     }
   }
   prefetch_l1<K>(xnext, R, wave, lane);
