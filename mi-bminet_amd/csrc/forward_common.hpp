@@ -53,6 +53,14 @@ struct SmallParams {
   int l4_thr[F2];
   int l4_off[F2];
   float l4_r[F2];
+  // plain (non-REORDER_BN) layer-2/4 branches: per-element BN with offset >> 3 and factor >> 3,
+  // as magic-offset MFMA C-init (offset + FMAGIC_I), reciprocal and -(1.5 * 2^23) * r
+  int l2n_ci[F2];
+  float l2n_r[F2];
+  float l2n_c[F2];
+  int l4n_ci[F2];
+  float l4n_r[F2];
+  float l4n_c[F2];
   int l5_w[N_OUT][ND5_MAX];  // flattened [k][v] order, zero padded
   int l5_b[N_OUT];
   float l3_r;

@@ -40,9 +40,10 @@ constexpr int WPE = 4;                // waves per SIMD (two workgroups per CU)
 constexpr int PF_MAX = 9;             // layer-1 blocks per wave prefetched one trial ahead
 static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wave");
 
-template <int C_, int T_>
+template <int C_, int T_, bool RB_ = true>
 struct Cfg {
   static constexpr int C = C_, T = T_;
+  static constexpr bool RB = RB_;                       // -DREORDER_BN variant (canonical)
   static constexpr int P = (C <= 32) ? 2 : 1;          // samples per 64-byte L1 window
   static constexpr int GS = P * C;                      // bytes per time group
   static constexpr int NB1 = (T + 16 * P - 1) / (16 * P);  // L1 blocks of 16 groups
@@ -117,7 +118,7 @@ struct Regs {
   __device__ __forceinline__ const L1Tile& tile(int t) const { return t == 0 ? t0 : t1; }
   __device__ __forceinline__ L1Tile& tile(int t) { return t == 0 ? t0 : t1; }
   v4i af[FPW][3];          // layer-2 band fragments of the wave's filters
-  int thr2[FPW], off2[FPW];
+  int thr2[FPW], off2[FPW];  // REORDER_BN: threshold, offset; plain: MFMA C-init, magic c bits
   float r2[FPW];
   long a3[FPW];            // layer-3 band fragments of the wave's filters
   v4i pf[K::PF];           // layer-1 fragments prefetched one trial ahead
@@ -191,9 +192,15 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
     const int f = wave * FPW + fi;
 #pragma unroll
     for (int s = 0; s < 3; s++) R.af[fi][s] = prm->l2_afrag[f][s][lane];
-    R.thr2[fi] = prm->l2_thr[f];
-    R.off2[fi] = prm->l2_off[f];
-    R.r2[fi] = prm->l2_r[f];
+    if constexpr (K::RB) {
+      R.thr2[fi] = prm->l2_thr[f];
+      R.off2[fi] = prm->l2_off[f];
+      R.r2[fi] = prm->l2_r[f];
+    } else {
+      R.thr2[fi] = prm->sp.l2n_ci[f];
+      R.off2[fi] = __float_as_int(prm->sp.l2n_c[f]);
+      R.r2[fi] = prm->sp.l2n_r[f];
+    }
     R.a3[fi] = prm->l3_afrag[f][lane];
   }
   // small parameters -> LDS
@@ -267,6 +274,27 @@ __device__ __forceinline__ void layer1(const int8_t* __restrict__ xt, const int8
 }
 
 // ---- layer 2 ---------------------------------------------------------------------------------
+// Plain (non-REORDER_BN) branch, layer2.c:139-210: each element requantised and clipped
+// (func_xcorr_scale -> transform.c:224), ReLU, sum of 8, >> 3.  acc holds the elements as
+// float bits (C-init = offset + FMAGIC_I), so q = fma(bits, r, c) = RN((x + off) * r);
+// med3(trunc(q), 0, 127) is clip-then-ReLU in one instruction.
+__device__ __forceinline__ unsigned l2n_out(const v16i& acc, float r, float c) {
+  int s[2];
+#pragma unroll
+  for (int w = 0; w < 2; w++) {
+    int e[8];
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      const f2 q = __builtin_elementwise_fma((f2){__int_as_float(acc[8 * w + i]), __int_as_float(acc[8 * w + i + 1])},
+                                             (f2){r, r}, (f2){c, c});
+      e[i] = (int)__builtin_amdgcn_fmed3f(q[0], 0.0f, 127.0f);  // trunc(clamp) == clamp(trunc)
+      e[i + 1] = (int)__builtin_amdgcn_fmed3f(q[1], 0.0f, 127.0f);
+    }
+    s[w] = ((e[0] + e[1] + e[2]) + (e[3] + e[4]) + (e[5] + e[6])) + e[7];
+  }
+  return (unsigned)(s[0] >> 3) | ((unsigned)(s[1] >> 3) << 8);
+}
+
 // Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].
 __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, float r) {
   const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r, r};
@@ -285,12 +313,15 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
     for (int fi = 0; fi < FPW; fi++) {
       const int f = wave * FPW + fi;
       const int8_t* pb = smem_y1 + f * K::Y1ROW + (32 / K::P) * (32 * mt + c);
-      v16i acc = {};
+      v16i acc;
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = K::RB ? 0 : R.thr2[fi];  // plain branch: C-init
 #pragma unroll
       for (int s = 0; s < 3; s++)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, h)), acc, 0, 0, 0);
       // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
-      const unsigned w = l2_out(acc, R.thr2[fi], R.off2[fi], R.r2[fi]);
+      const unsigned w = K::RB ? l2_out(acc, R.thr2[fi], R.off2[fi], R.r2[fi])
+                               : l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
       const int u0 = 4 * (32 * mt + c) + 2 * h;
       int8_t* dst = smem_y2 + f * K::Y2ROW + 8 + u0;
       if (128 * (mt + 1) <= K::T8 || u0 + 1 < K::T8) *(unsigned short*)dst = (unsigned short)w;
@@ -298,7 +329,11 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
     }
   if constexpr (K::TB > 0) {
     const int fi_c = c / K::TB, b = c % K::TB;  // this lane's tail column: filter slot, block
-    v16i tacc = {};
+    const bool cvalid = fi_c < FPW;
+    const int fcol = wave * FPW + (cvalid ? fi_c : 0);  // filter of this lane's tail column
+    v16i tacc;
+#pragma unroll
+    for (int i = 0; i < 16; i++) tacc[i] = K::RB ? 0 : sp->l2n_ci[fcol];
 #pragma unroll
     for (int fi = 0; fi < FPW; fi++) {
       const int f = wave * FPW + fi;
@@ -308,9 +343,10 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
       for (int s = 0; s < 3; s++)
         tacc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, h)), tacc, 0, 0, 0);
     }
-    const bool valid = fi_c < FPW;
-    const int fc = wave * FPW + (valid ? fi_c : 0);
-    const unsigned w = l2_out(tacc, sp->l2_thr[fc], sp->l2_off[fc], sp->l2_r[fc]);
+    const bool valid = cvalid;
+    const int fc = fcol;
+    const unsigned w = K::RB ? l2_out(tacc, sp->l2_thr[fc], sp->l2_off[fc], sp->l2_r[fc])
+                             : l2n_out(tacc, sp->l2n_r[fc], sp->l2n_c[fc]);
     const int u0 = 4 * (32 * K::MT + b) + 2 * h;
     if (valid && u0 < K::T8) {
       int8_t* dst = smem_y2 + fc * K::Y2ROW + 8 + u0;
@@ -376,10 +412,34 @@ __device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, c
   for (int t = 0; t < K::NT4; t++) a[t] = *(const v4i*)(smem_y3 + (64 * t + 32 * h + n) * K::Y3S);  // unaligned (4 B)
 #pragma unroll
   for (int t = 0; t < K::NT4; t++) {
-    v16i acc = {};
+    v16i acc;
+#pragma unroll
+    for (int j = 0; j < 16; j++) acc[j] = K::RB ? 0 : sp->l4n_ci[k];  // plain branch: C-init
     acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[t], bw, acc, 0, 0, 0);
-    const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
-    const unsigned w = sat8x2((int)q[0], (int)q[1]);
+    unsigned w;
+    if constexpr (K::RB) {
+      const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
+      w = sat8x2((int)q[0], (int)q[1]);
+    } else {
+      // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
+      // sum of 8, >> 3, clip.  Elements are clamped to [0, 1024]: any element >= 1024 already
+      // saturates the result, and the reciprocal is verified exact up to there.
+      const float rn = sp->l4n_r[k], cn = sp->l4n_c[k];
+      int sm[2];
+#pragma unroll
+      for (int hw = 0; hw < 2; hw++) {
+        int e[8];
+#pragma unroll
+        for (int j = 0; j < 8; j += 2) {
+          const f2 q = __builtin_elementwise_fma((f2){__int_as_float(acc[8 * hw + j]), __int_as_float(acc[8 * hw + j + 1])},
+                                                 (f2){rn, rn}, (f2){cn, cn});
+          e[j] = (int)__builtin_amdgcn_fmed3f(q[0], 0.0f, 1024.0f);
+          e[j + 1] = (int)__builtin_amdgcn_fmed3f(q[1], 0.0f, 1024.0f);
+        }
+        sm[hw] = min((((e[0] + e[1] + e[2]) + (e[3] + e[4]) + (e[5] + e[6])) + e[7]) >> 3, 127);
+      }
+      w = (unsigned)sm[0] | ((unsigned)sm[1] << 8);
+    }
     const int v0 = 8 * t + 4 * (i >> 4) + 2 * h;
     int8_t* dst = smem_y4 + k * K::T64 + v0;
     if (v0 < K::T64) dst[0] = (int8_t)w;

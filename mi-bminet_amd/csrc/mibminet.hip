@@ -8,6 +8,7 @@
 // There is no CPU compute path: without a usable HIP device every entry point returns an error.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -45,6 +46,7 @@ struct HostParams {
   std::vector<int32_t> l1_factor, l1_offset, l2_factor, l2_offset, l4_factor, l4_offset;
   std::vector<int8_t> l1_weight_align, l2_weight_reverse, l3_weight, l4_weight, l5_bias, l5_weight;
   int32_t l3_factor = 0, l5_factor = 0;
+  bool reorder_bn = true;  // blob flag: -DREORDER_BN variant (canonical) or the plain BN branches
 };
 
 // ---- exact requantisation ------------------------------------------------------------------
@@ -59,9 +61,12 @@ inline int64_t trunc_div(int64_t a, int64_t b) { return a / b; }  // C semantics
 
 inline int64_t qf(int64_t v, float r) { return (int64_t)(int32_t)((float)v * r); }
 
-bool verify_reciprocal(int32_t fac, float r) {
+// kmax: largest output step that must be exact (128 for int8 clipping; the non-REORDER_BN
+// layer 4 clamps its unclipped elements at 1024 instead).  vmax: largest reachable |v|;
+// intervals beyond it are not checked.
+bool verify_reciprocal(int32_t fac, float r, int64_t kmax = 128, int64_t vmax = (1 << 24) - 1) {
   const int64_t F = fac < 0 ? -(int64_t)fac : (int64_t)fac;
-  for (int64_t k = -129; k <= 128; k++) {
+  for (int64_t k = -129; k <= kmax; k++) {
     // interval of v (for |fac|) with trunc(v / F) == k
     int64_t lo, hi;
     if (k > 0) { lo = k * F; hi = k * F + F - 1; }
@@ -72,6 +77,9 @@ bool verify_reciprocal(int32_t fac, float r) {
       lo = a; hi = b;
     }
     const int64_t want = k;
+    if (lo > vmax || hi < -vmax) continue;  // unreachable
+    lo = std::max(lo, -vmax);
+    hi = std::min(hi, vmax);
     if (std::llabs(lo) >= (1 << 24) || std::llabs(hi) >= (1 << 24)) return false;
     if (qf(lo, r) != want || qf(hi, r) != want) return false;
     if (trunc_div(lo, fac) != want || trunc_div(hi, fac) != want) return false;  // self-check
@@ -79,7 +87,8 @@ bool verify_reciprocal(int32_t fac, float r) {
   return true;
 }
 
-bool choose_reciprocal(int32_t fac, float* out, float* magic_c = nullptr) {
+bool choose_reciprocal(int32_t fac, float* out, float* magic_c = nullptr, int64_t kmax = 128,
+                       int64_t vmax = (1 << 24) - 1) {
   // magic_c != nullptr: additionally require c = -(1.5 * 2^23) * r to be exact in f32, so that
   // fma(bits_as_float(v + 0x4B400000), r, c) == RN(v * r) (layer 1's one-instruction requant).
   if (fac == 0) return false;
@@ -96,7 +105,7 @@ bool choose_reciprocal(int32_t fac, float* out, float* magic_c = nullptr) {
       ok = ((double)cf == cd);
       if (ok) *magic_c = cf;
     }
-    if (ok && verify_reciprocal(fac, rs)) { *out = rs; return true; }
+    if (ok && verify_reciprocal(fac, rs, kmax, vmax)) { *out = rs; return true; }
     r = std::nextafterf(r, INFINITY);
   }
   return false;
@@ -155,7 +164,7 @@ int parse_blob(const void* blob, size_t len, HostParams& hp) {
   d.N = (int)h[6]; d.wbits = (int)h[7];
   const uint32_t l2t = h[8], l3t = h[9], flags = h[10];
   if (version != 1 || l2t != 64 || l3t != 16) return NET_ERR_BLOB;
-  if (!(flags & FLAG_REORDER_BN)) return NET_ERR_UNSUPPORTED;
+  hp.reorder_bn = (flags & FLAG_REORDER_BN) != 0;
   if (d.wbits != 8 && d.wbits != 4) return NET_ERR_BLOB;
   if (d.C <= 0 || d.T < 64 || d.F1 <= 0 || d.N <= 0 || d.F2 != d.F1 * d.D) return NET_ERR_BLOB;
   Reader r{b, len, (size_t)HEADER_SIZE};
@@ -193,6 +202,21 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     if (std::llabs((int64_t)hp.l4_offset[f]) + 8LL * F2 * A >= (1 << 24)) return NET_ERR_RANGE;
   }
   if (128LL + (int64_t)F2 * d.T64() * A >= (1 << 24)) return NET_ERR_RANGE;
+  if (!hp.reorder_bn) {
+    // plain branches: per-element BN with offset >> 3 and factor >> 3 through the magic-offset
+    // C-init (|x + off| < 2^22); layer 4's elements are exact up to the 1024 clamp
+    for (int f = 0; f < F2; f++) {
+      const int32_t f2 = hp.l2_factor[f] >> 3, o2 = hp.l2_offset[f] >> 3;
+      const int32_t f4 = hp.l4_factor[f] >> 3, o4 = hp.l4_offset[f] >> 3;
+      if (f2 == 0 || f4 == 0) return NET_ERR_RANGE;
+      const int64_t v2 = 64LL * A + std::llabs((int64_t)o2), v4 = (int64_t)F2 * A + std::llabs((int64_t)o4);
+      if (v2 >= (1 << 22) || v4 >= (1 << 22)) return NET_ERR_RANGE;
+      dp.sp.l2n_ci[f] = o2 + FMAGIC_I;
+      dp.sp.l4n_ci[f] = o4 + FMAGIC_I;
+      if (!choose_reciprocal(f2, &dp.sp.l2n_r[f], &dp.sp.l2n_c[f], 128, v2)) return NET_ERR_RANGE;
+      if (!choose_reciprocal(f4, &dp.sp.l4n_r[f], &dp.sp.l4n_c[f], 1025, v4)) return NET_ERR_RANGE;
+    }
+  }
   // layer 1: B operand (column j of N-tile t: filter 8t + j/2, parity j&1 when P == 2)
   for (int t = 0; t < P; t++) {
     for (int lane = 0; lane < 64; lane++) {
@@ -288,12 +312,15 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
 // ---- compiled configurations --------------------------------------------------------------
 using CfgB = wg::Cfg<22, 1125>;  // BCI-IV-2a: 22 channels x 1125 samples (configs A, B, D, E)
 using CfgC = wg::Cfg<64, 1000>;  // high-density variant: 64 channels x 1000 samples (config C)
+using CfgBn = wg::Cfg<22, 1125, false>;  // the same networks built without -DREORDER_BN
+using CfgCn = wg::Cfg<64, 1000, false>;
 
-enum class Variant { None, B22x1125, C64x1000 };
+enum class Variant { None, B22x1125, C64x1000, B22x1125n, C64x1000n };
 
-Variant variant_of(const Dims& d) {
-  if (d.C == 22 && d.T == 1125) return Variant::B22x1125;
-  if (d.C == 64 && d.T == 1000) return Variant::C64x1000;
+Variant variant_of(const HostParams& hp) {
+  const Dims& d = hp.d;
+  if (d.C == 22 && d.T == 1125) return hp.reorder_bn ? Variant::B22x1125 : Variant::B22x1125n;
+  if (d.C == 64 && d.T == 1000) return hp.reorder_bn ? Variant::C64x1000 : Variant::C64x1000n;
   return Variant::None;
 }
 
@@ -396,6 +423,8 @@ int launch_forward(Variant v, DeviceState& ds, const DevParams* p, const int8_t*
   switch (v) {
     case Variant::B22x1125: return launch_forward_t<CfgB>(ds, p, x, y, B, st, info);
     case Variant::C64x1000: return launch_forward_t<CfgC>(ds, p, x, y, B, st, info);
+    case Variant::B22x1125n: return launch_forward_t<CfgBn>(ds, p, x, y, B, st, info);
+    case Variant::C64x1000n: return launch_forward_t<CfgCn>(ds, p, x, y, B, st, info);
     default: return NET_ERR_UNSUPPORTED;
   }
 }
@@ -407,6 +436,12 @@ int launch_layer(Variant v, const DevParams* p, const int8_t* in, int8_t* out, i
       break;
     case Variant::C64x1000:
       hipLaunchKernelGGL(wg::k_layer<CfgC>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
+      break;
+    case Variant::B22x1125n:
+      hipLaunchKernelGGL(wg::k_layer<CfgBn>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
+      break;
+    case Variant::C64x1000n:
+      hipLaunchKernelGGL(wg::k_layer<CfgCn>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
       break;
     default: return NET_ERR_UNSUPPORTED;
   }
@@ -420,7 +455,7 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
   const Dims& d = s.host->d;
-  const Variant v = variant_of(d);
+  const Variant v = variant_of(*s.host);
   if (v == Variant::None) return NET_ERR_UNSUPPORTED;
   const int dev = g_single_device;
   DeviceState& ds = g_devs[dev];
@@ -499,7 +534,7 @@ int net_params_load(const void* blob, size_t len) {
   auto hp = std::make_shared<HostParams>();
   int rc = parse_blob(blob, len, *hp);
   if (rc) return rc;
-  if (variant_of(hp->d) == Variant::None) return NET_ERR_UNSUPPORTED;
+  if (variant_of(*hp) == Variant::None) return NET_ERR_UNSUPPORTED;
   auto dp = std::make_shared<DevParams>();
   rc = build_devparams(*hp, *dp);
   if (rc) return rc;
@@ -549,7 +584,7 @@ int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int devi
   if (device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
-  const Variant v = variant_of(s.host->d);
+  const Variant v = variant_of(*s.host);
   if (v == Variant::None) return NET_ERR_UNSUPPORTED;
   DeviceState& ds = g_devs[device];
   std::lock_guard<std::mutex> lk(ds.mu);
@@ -578,7 +613,7 @@ int net_launch_info(size_t B, int device, int32_t* out) {
   if (!out || device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
-  const Variant v = variant_of(s.host->d);
+  const Variant v = variant_of(*s.host);
   DeviceState& ds = g_devs[device];
   std::lock_guard<std::mutex> lk(ds.mu);
   DeviceGuard guard(device);

@@ -71,6 +71,11 @@ def layer2(p, y1: np.ndarray) -> np.ndarray:
     """Layer2.__call__ reorder_bn=True (golden_model.py:241-247): conv_time, relu(-(bias//8)),
     sum-pool 8, apply_factor_offset.  [B, F2, T] -> [B, F2, T//8]."""
     a = xcorr_same(y1, p.l2_weight_reverse, 31, 32)
+    if not getattr(p, "reorder_bn", True):
+        # reorder_bn=False (golden_model.py:248-251): BN per element with factor//8, bias//8
+        # (clip), relu at 0, sum-pool 8, // 8
+        y = apply_factor_offset(a, p.l2_factor.astype(np.int64) // 8, p.l2_offset.astype(np.int64) // 8)
+        return pool(np.maximum(y, 0), 8) // 8
     thr = -(p.l2_offset.astype(np.int64) // 8)
     return apply_factor_offset(pool(relu(a, thr), 8), p.l2_factor, p.l2_offset)
 
@@ -85,6 +90,12 @@ def layer4(p, y3: np.ndarray) -> np.ndarray:
     """Layer4.__call__ reorder_bn=True (golden_model.py:330-337): pointwise_conv, relu, pool 8,
     apply_factor_offset.  [B, F2, T8] -> [B, F2, T64]."""
     b = np.einsum("bft,kf->bkt", y3.astype(np.int64), p.l4_weight.astype(np.int64), optimize=True)
+    if not getattr(p, "reorder_bn", True):
+        # reorder_bn=False (golden_model.py:337-340).  NB: the golden model clips each element to
+        # int8 before the ReLU, the reference C (layer4.c:113-118) does not; the two only differ
+        # when an element exceeds 127 (tests/test_variants.py pins both behaviours).
+        y = apply_factor_offset(b, p.l4_factor.astype(np.int64) // 8, p.l4_offset.astype(np.int64) // 8)
+        return pool(np.maximum(y, 0), 8) // 8
     thr = -(p.l4_offset.astype(np.int64) // 8)
     return apply_factor_offset(pool(relu(b, thr), 8), p.l4_factor, p.l4_offset)
 

@@ -63,17 +63,32 @@ void or_layer2(const or_params_t* p, const int8_t* y1, int8_t* y2) {
             xc[i] = acc;
         }
         const int32_t fac = p->l2_factor[f], off = p->l2_offset[f];
-        const int32_t thr = -(off >> 3);
         const int32_t* it = xc;
-        for (int u = 0; u < p->T8; u++) {
-            int32_t sum = 0;
-            for (int k = 0; k < 8; k++) {
-                int32_t v = *(it++);
-                sum += v > thr ? v : thr; /* __MAX */
+        if (p->reorder_bn) {
+            const int32_t thr = -(off >> 3);
+            for (int u = 0; u < p->T8; u++) {
+                int32_t sum = 0;
+                for (int k = 0; k < 8; k++) {
+                    int32_t v = *(it++);
+                    sum += v > thr ? v : thr; /* __MAX */
+                }
+                sum = sum + off;
+                sum = sum / fac;
+                y2[(size_t)f * p->T8_ALIGN + u] = (int8_t)clip8(sum);
             }
-            sum = sum + off;
-            sum = sum / fac;
-            y2[(size_t)f * p->T8_ALIGN + u] = (int8_t)clip8(sum);
+        } else {
+            /* layer2.c:139-210: factor and offset >> 3, func_xcorr_scale (xcorr.c:346 ->
+             * transform.c:224: clip((x + offset) / factor) to int8), then sum of 8 ReLUs >> 3, clip */
+            const int32_t fac3 = fac >> 3, off3 = off >> 3;
+            for (int u = 0; u < p->T8; u++) {
+                int32_t sum = 0;
+                for (int k = 0; k < 8; k++) {
+                    int32_t v = clip8((*(it++) + off3) / fac3);
+                    sum += v > 0 ? v : 0;
+                }
+                sum = sum >> 3;
+                y2[(size_t)f * p->T8_ALIGN + u] = (int8_t)clip8(sum);
+            }
         }
     }
     free(xc);
@@ -120,18 +135,29 @@ void or_layer4(const or_params_t* p, const int8_t* y3t, int8_t* y4) {
     for (int k = 0; k < p->F2; k++) {
         const int32_t fac = p->l4_factor[k], off = p->l4_offset[k];
         const int32_t thr = -(off >> 3);
+        const int32_t fac3 = fac >> 3, off3 = off >> 3;
         const int8_t* w = p->l4_weight + (size_t)k * p->F2;
         const int8_t* it = y3t;
         for (int v = 0; v < p->T64; v++) {
             int32_t sum = 0;
             for (int i = 0; i < 8; i++) {
                 int32_t e = dotp(it, w, p->F2);
-                e = e > thr ? e : thr;
+                if (p->reorder_bn) {
+                    e = e > thr ? e : thr;
+                } else {
+                    /* layer4.c:113-118: BN per element (no clip), then ReLU */
+                    e = (e + off3) / fac3;
+                    e = e > 0 ? e : 0;
+                }
                 sum += e;
                 it += p->F2;
             }
-            sum = sum + off;
-            sum = sum / fac;
+            if (p->reorder_bn) {
+                sum = sum + off;
+                sum = sum / fac;
+            } else {
+                sum = sum >> 3;  /* layer4.c:130 */
+            }
             y4[(size_t)k * p->T64_ALIGN + v] = (int8_t)clip8(sum);
         }
     }

@@ -2,8 +2,8 @@
  * oracle.h — TEST INFRASTRUCTURE ONLY.
  *
  * Plain-C restatement of the reference's canonical integer forward pass
- * (edge-eegnet_wolf/src/cl/net/layer{1..5}.c with -DPARALLEL -DCROSS_CORRELATE -DREORDER_BN -DFLIP_LAYERS,
- * serialised).  It is the checker for the HIP path: only tests/, __graft_entry__.smoke() and the
+ * (edge-eegnet_wolf/src/cl/net/layer{1..5}.c with -DPARALLEL -DCROSS_CORRELATE -DFLIP_LAYERS, and
+ * either -DREORDER_BN (canonical) or not (or_params_t.reorder_bn), serialised).  It is the checker for the HIP path: only tests/, __graft_entry__.smoke() and the
  * cpu_baseline leg of bench.py may load it.  The product library (libmibminet.so) never links or
  * calls it.
  *
@@ -48,6 +48,7 @@ typedef struct {
     int32_t        l5_factor;
     const int8_t*  l5_bias;         /* [N] */
     const int8_t*  l5_weight;       /* [N][F2*T64_ALIGN] */
+    int32_t        reorder_bn;      /* 1: -DREORDER_BN branches (canonical), 0: the plain ones */
 } or_params_t;
 
 void or_layer1(const or_params_t* p, const int8_t* x, int8_t* y1);
