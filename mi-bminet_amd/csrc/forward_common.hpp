@@ -65,7 +65,8 @@ struct SmallParams {
   int l5_b[N_OUT];
   float l3_r;
   float l5_r;
-  int pad[2];
+  float l3_c;             // -(1.5 * 2^23) * l3_r (layer 3's magic C-init requant)
+  int pad[1];
 };
 
 // Operand fragments and requantisation constants, built by the host from the net.h arrays.
@@ -79,6 +80,7 @@ struct DevParams {
   int l2_off[F2];
   float l2_r[F2];
   long l3_afrag[F2][64];    // layer-3 A operand (16 shifts x 32-byte band) per filter and lane
+  v4i l2t_afrag[F2][2][64]; // layer-2 tail A operand (16 shifts x 128-slot band, MFMA 16x16x64)
   SmallParams sp;
 };
 

@@ -13,10 +13,11 @@
 //   layer2  64-tap depthwise temporal xcorr as a banded-Toeplitz GEMM on MFMA i32_32x32x32_i8:
 //           A = 32 output shifts x 96-tap band of the filter (held in registers; rows permuted so
 //           that each lane owns two whole pool-8 windows), B = 16-byte slices of the layer-1 row
-//           at immediate offsets.  32 column blocks per filter form its full tile; the TB
-//           remaining blocks of the wave's FPW filters share one tail tile (block-diagonal K:
-//           each filter's MFMAs read the zero row for the other filter's columns), so the
-//           ReLU / sum-pool 8 / requant VALU work is not spent on empty columns.
+//           at immediate offsets.  32 column blocks per filter form its full tile.  The 32 TB
+//           outputs left per filter run on MFMA i32_16x16x64_i8 (16 shifts x 128-slot band, A
+//           from LDS): columns of 16 outputs, the wave's FPW filters side by side (block-diagonal
+//           K: each filter's MFMAs read the zero row for the other filter's columns); a lane
+//           holds half a pool window, the two halves meet by v_permlane16_swap.
 //                                                    (reference: layer2.c:56-118, xcorr.c:44)
 //   layer3  16-tap depthwise conv on MFMA i32_16x16x32_i8: A = 16 shifts x 32-byte band of the
 //           filter (registers), B = aligned 8-byte slices of the layer-2 row (columns = blocks of
@@ -40,6 +41,30 @@ constexpr int WPE = 4;                // waves per SIMD (two workgroups per CU)
 constexpr int PF_MAX = 9;             // layer-1 blocks per wave prefetched one trial ahead
 static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wave");
 
+// Layer-1 work split.  The last wave also runs layers 4 and 5 (in the same barrier interval as
+// the next trial's layer 1), so it takes fewer layer-1 blocks: waves 0 .. NWAVES-2 get cm blocks
+// (the first rm of them one more), the last wave cl, with layers 4-5 counted as W45 blocks.
+#ifndef MIB_W45
+#define MIB_W45 4
+#endif
+struct L1Split {
+  int cm, rm, cl;
+};
+constexpr L1Split l1_split(int nb1) {
+  constexpr int nm = NWAVES - 1;
+  L1Split best{0, 0, 0};
+  int bcost = 1 << 30;
+  for (int cl = 0; cl <= nb1; cl++) {
+    const int cm = (nb1 - cl) / nm, rm = (nb1 - cl) % nm;
+    const int hi = cmax(cm + (rm ? 1 : 0), cl + MIB_W45);
+    if (hi < bcost) {
+      bcost = hi;
+      best = L1Split{cm, rm, cl};
+    }
+  }
+  return best;
+}
+
 template <int C_, int T_, bool RB_ = true>
 struct Cfg {
   static constexpr int C = C_, T = T_;
@@ -47,19 +72,15 @@ struct Cfg {
   static constexpr int P = (C <= 32) ? 2 : 1;          // samples per 64-byte L1 window
   static constexpr int GS = P * C;                      // bytes per time group
   static constexpr int NB1 = (T + 16 * P - 1) / (16 * P);  // L1 blocks of 16 groups
-  // layer-1 block split.  SPLIT: waves 0..NWAVES-2 take NBM blocks each (round robin) and the
-  // last wave, which also runs layers 4-5 at the end of the trial, takes the NL leftover
-  // blocks.  Otherwise plain round robin over all waves.
-  static constexpr bool SPLIT = NB1 % (NWAVES - 1) != 0 && NB1 % (NWAVES - 1) < NB1 / NWAVES;
-  static constexpr int NLW = SPLIT ? NWAVES - 1 : NWAVES;
-  static constexpr int NL = SPLIT ? NB1 % NLW : 0;
-  static constexpr int NBM = SPLIT ? (NB1 - NL) / NLW : (NB1 + NWAVES - 1) / NWAVES;
-  static constexpr int NBW = cmax(NBM, NL);             // L1 blocks per wave (max)
-  static constexpr int PF = cmin(NBW, PF_MAX);          // of which prefetched a trial ahead
   static constexpr int T8 = T / 8, T64 = T8 / 8;
+  static constexpr int NT4 = (8 * T64 + 63) / 64;       // L4 MFMAs of 64 time samples
+  static constexpr L1Split SPL = l1_split(NB1);
+  static constexpr int NBW = cmax(SPL.cm + (SPL.rm ? 1 : 0), SPL.cl);  // L1 blocks per wave (max)
+  static constexpr int PF = cmin(NBW, PF_MAX);          // of which prefetched a trial ahead
   static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
   static constexpr int MT = NB2 / 32;                   // full L2 tiles per filter
-  static constexpr int TB = NB2 - 32 * MT;              // tail blocks per filter
+  static constexpr int TB = NB2 - 32 * MT;              // tail blocks (of 32 outputs) per filter
+  static constexpr int TC = 2 * TB;                     // tail columns (of 16 outputs) per filter
   // layer-1 rows hold positions pos = t + 32 (32 leading zeros = the xcorr pad of 31, aligned).
   // P == 2: parity-split planes [pos & 1][pos >> 1]: each lane's 4 outputs (one parity) are
   // contiguous and layer 2's K-window slices are 16-B aligned.
@@ -69,7 +90,6 @@ struct Cfg {
   static constexpr int XTRIAL = align16(T * C);         // batched trial stride (bytes)
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   static constexpr int Y2ROW = odd_dwords(cmax(T8 + 24, 16 * NB3 + 24));
-  static constexpr int NT4 = (8 * T64 + 63) / 64;       // L4 MFMAs of 64 time samples
   static constexpr int Y3ROWS = cmax(64 * NT4, T8);
   // y3t rows are 20 bytes apart (16 filters + 4 pad): layer 3's 2-byte stores from 64 lanes
   // (64 different rows) then hit 64 different banks; layer 4 reads a row with one unaligned
@@ -84,13 +104,14 @@ struct Cfg {
   static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S);
   static constexpr int OFF_ZERO = OFF_Y4 + align16(64 * N5L);
   static constexpr int OFF_SP = OFF_ZERO + 128;
-  static constexpr int LDS = align16(OFF_SP + (int)sizeof(SmallParams));
+  static constexpr int OFF_L2T = align16(OFF_SP + (int)sizeof(SmallParams));  // tail band fragments
+  static constexpr int LDS = OFF_L2T + (TB > 0 ? F2 * 2 * 64 * 16 : 0);
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
   static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
   static_assert(T64 >= 1, "T >= 64");
   static_assert(16 * N5L <= ND5_MAX, "layer-5 input too long");
   static_assert(MT >= 1, "at least one full layer-2 tile");
-  static_assert(FPW * TB <= 32, "tail columns of a wave fit one tile");
+  static_assert(FPW * TC <= 16, "tail columns of a wave fit one 16-column tile");
   static_assert(OFF_ZERO >= F2 * Y1ROW, "zero-row addressing stays non-negative");
 };
 
@@ -155,19 +176,25 @@ __device__ __forceinline__ v4i fix_a(v4i v, int blk, int lane) {
   return r;
 }
 
-// i-th layer-1 block of a wave (the last wave's unused slots repeat its last block: the loads
-// stay unconditional, the compute is skipped)
+// Layer-1 blocks of a wave: a contiguous range (see l1_split).  Slots past the wave's count
+// repeat its last block (the loads stay unconditional, the compute is skipped).
 template <class K>
-__device__ __forceinline__ int l1_blk(int wave, int i) {
-  if (!K::SPLIT) return min(wave + NWAVES * i, K::NB1 - 1);
-  if (wave < K::NLW) return wave + K::NLW * i;
-  return K::NB1 - K::NL + min(i, K::NL - 1);
+__device__ __forceinline__ int l1_count(int wave) {
+  constexpr L1Split S = K::SPL;
+  return wave < NWAVES - 1 ? S.cm + (wave < S.rm) : S.cl;
 }
 
 template <class K>
-__device__ __forceinline__ int l1_count(int wave) {
-  if (!K::SPLIT) return (K::NB1 - wave + NWAVES - 1) / NWAVES;
-  return wave < K::NLW ? K::NBM : K::NL;
+__device__ __forceinline__ int l1_start(int wave) {
+  constexpr L1Split S = K::SPL;
+  return wave * S.cm + min(wave, S.rm);
+}
+
+template <class K>
+__device__ __forceinline__ int l1_blk(int wave, int i) {
+  const int n = l1_count<K>(wave);
+  const int b = l1_start<K>(wave) + (i < n ? i : n - 1);
+  return b < 0 ? 0 : (b > K::NB1 - 1 ? K::NB1 - 1 : b);
 }
 
 template <class K>
@@ -207,6 +234,11 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   const v4i* src = (const v4i*)&prm->sp;
   v4i* dst = (v4i*)(smem + K::OFF_SP);
   for (int i = tid; i < (int)(sizeof(SmallParams) / 16); i += NTHREADS) dst[i] = src[i];
+  if constexpr (K::TB > 0) {
+    const v4i* t = &prm->l2t_afrag[0][0][0];
+    v4i* d = (v4i*)(smem + K::OFF_L2T);
+    for (int i = tid; i < F2 * 2 * 64; i += NTHREADS) d[i] = t[i];
+  }
   // everything else zero: layer-1 pads (positions [0,32) and past the last block), layer-2 pads
   // ([0,8) and [8+T8, Y2ROW)) and the zero row are never rewritten
   v4i* z = (v4i*)smem;
@@ -229,6 +261,14 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
   for (int t = 0; t < K::P; t++) {
     const L1Tile& T = R.tile(t);
     const v4i acc = accs[t];
+#ifdef MIB_DIAG_NOL1RQ
+    {
+      const int p = (K::P == 2) ? (j & 1) : 0;
+      const int f = (K::P == 2) ? 8 * t + (j >> 1) : j;
+      *(unsigned*)(smem_y1 + y1_index<K>(f, K::P * (16 * blk + 4 * g) + p)) = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
+      continue;
+    }
+#endif
     // acc bits = 1.5*2^23 + (dot + off) as f32; fma(x, r, -1.5*2^23*r) == RN((dot+off)*r)
     const f2 rr2 = {T.rr, T.rr}, cc2 = {T.cc, T.cc};
     const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(acc[0]), __int_as_float(acc[1])}, rr2, cc2);
@@ -301,12 +341,80 @@ __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, fl
   return sat8x2((int)q[0], (int)q[1]);
 }
 
+// Layer-2 tail: outputs 1024 MT + 16 bq + m (m < 16) of the wave's filters on MFMA
+// i32_16x16x64_i8.  Column col = TC fi + bq; A = the filter's 16-shift band (LDS, [f][s][lane]);
+// B lane (col, g), K-step s = 16 bytes of the column's 128-position window (P == 2: plane g >> 1,
+// plane bytes 32 s + 16 (g & 1) .. +15, 8-byte aligned).  Slots past window position 79 meet zero
+// weights, so the window may run into the next plane / row.  D lane (col, g) holds shifts
+// 4g .. 4g+3: half of pool window g >> 1; lanes g and g ^ 1 are rows 2k, 2k+1 of the wave and
+// meet by v_permlane16_swap.
+template <class K>
+__device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const int8_t* zero, const SmallParams* sp,
+                                                int wave, int lane) {
+  const int col = lane & 15, g = lane >> 4;
+  const int fi_c = col / K::TC, bq = col - fi_c * K::TC;
+  const int fcol = wave * FPW + (fi_c < FPW ? fi_c : 0);
+  const v4i* tA = (const v4i*)(smem_y1 - K::OFF_Y1 + K::OFF_L2T);
+  constexpr int SOFF = K::P == 2 ? 32 : 64;  // B byte offset of K-step 1
+  const int boff = (K::P == 2) ? (g >> 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (g & 1)
+                               : 1024 * K::MT + 16 * bq + 16 * g;
+  v4i tacc;
+#pragma unroll
+  for (int i = 0; i < 4; i++) tacc[i] = K::RB ? 0 : sp->l2n_ci[fcol];
+#pragma unroll
+  for (int fi = 0; fi < FPW; fi++) {
+    const int f = wave * FPW + fi;
+    const int8_t* pb = (fi_c == fi) ? smem_y1 + f * K::Y1ROW + boff : zero + 16 * g;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const long* q = (const long*)(pb + SOFF * s);
+      const long lo = q[0], hi = q[1];
+      v4i bv;
+      bv[0] = (int)lo; bv[1] = (int)(lo >> 32); bv[2] = (int)hi; bv[3] = (int)(hi >> 32);
+      tacc = __builtin_amdgcn_mfma_i32_16x16x64_i8(tA[(2 * f + s) * 64 + lane], bv, tacc, 0, 0, 0);
+    }
+  }
+  return tacc;
+}
+
+template <class K>
+__device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2, const SmallParams* sp, int wave,
+                                                int lane) {
+  const int col = lane & 15, g = lane >> 4;
+  const int fi_c = col / K::TC, bq = col - fi_c * K::TC;
+  const bool cvalid = fi_c < FPW;
+  const int fcol = wave * FPW + (cvalid ? fi_c : 0);
+  int part;
+  if constexpr (K::RB) {
+    const int thr = sp->l2_thr[fcol];
+    part = (max(tacc[0], thr) + max(tacc[1], thr)) + (max(tacc[2], thr) + max(tacc[3], thr));
+  } else {
+    const float r = sp->l2n_r[fcol], c = sp->l2n_c[fcol];
+    const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(tacc[0]), __int_as_float(tacc[1])}, (f2){r, r}, (f2){c, c});
+    const f2 q23 = __builtin_elementwise_fma((f2){__int_as_float(tacc[2]), __int_as_float(tacc[3])}, (f2){r, r}, (f2){c, c});
+    part = ((int)__builtin_amdgcn_fmed3f(q01[0], 0.0f, 127.0f) + (int)__builtin_amdgcn_fmed3f(q01[1], 0.0f, 127.0f)) +
+           ((int)__builtin_amdgcn_fmed3f(q23[0], 0.0f, 127.0f) + (int)__builtin_amdgcn_fmed3f(q23[1], 0.0f, 127.0f));
+  }
+  const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)part, (unsigned)part, false, false);
+  const int tot = (int)sw[0] + (int)sw[1];  // whole window (rows 2k and 2k+1 hold the same)
+  int y;
+  if constexpr (K::RB) y = rq(tot + sp->l2_off[fcol], sp->l2_r[fcol]);
+  else y = tot >> 3;
+  const int u = 128 * K::MT + 2 * bq + (g >> 1);
+  if (cvalid && !(g & 1) && u < K::T8) smem_y2[fcol * K::Y2ROW + 8 + u] = (int8_t)y;
+}
+
 // Layer 2: y1 rows -> y2 rows (LDS, position 8 + u).  Full tiles of the wave's filters, then the
-// shared tail tile (filter fi's blocks 32 MT + b -> column TB fi + b).
+// tail (layer2_tail).
 template <class K>
 __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, const int8_t* zero,
                                        const SmallParams* sp, const Regs<K>& R, int wave, int lane) {
   const int c = lane & 31, h = lane >> 5;
+#if !defined(MIB_DIAG_NOTAIL) && defined(MIB_TAIL_FIRST)
+  // the tail's MFMAs first: their latency hides behind the full tiles
+  v4i tacc;
+  if constexpr (K::TB > 0) tacc = layer2_tail_mfma<K>(smem_y1, zero, sp, wave, lane);
+#endif
 #pragma unroll
   for (int mt = 0; mt < K::MT; mt++)
 #pragma unroll
@@ -320,39 +428,26 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
       for (int s = 0; s < 3; s++)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, h)), acc, 0, 0, 0);
       // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
+#ifdef MIB_DIAG_NOPOOL
+      const unsigned w = acc[0] ^ acc[5] ^ acc[10] ^ acc[15];
+#else
       const unsigned w = K::RB ? l2_out(acc, R.thr2[fi], R.off2[fi], R.r2[fi])
                                : l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
+#endif
       const int u0 = 4 * (32 * mt + c) + 2 * h;
       int8_t* dst = smem_y2 + f * K::Y2ROW + 8 + u0;
       if (128 * (mt + 1) <= K::T8 || u0 + 1 < K::T8) *(unsigned short*)dst = (unsigned short)w;
       else if (u0 < K::T8) *dst = (int8_t)w;
     }
+#ifdef MIB_DIAG_NOTAIL
+  if constexpr (false) {
+#else
   if constexpr (K::TB > 0) {
-    const int fi_c = c / K::TB, b = c % K::TB;  // this lane's tail column: filter slot, block
-    const bool cvalid = fi_c < FPW;
-    const int fcol = wave * FPW + (cvalid ? fi_c : 0);  // filter of this lane's tail column
-    v16i tacc;
-#pragma unroll
-    for (int i = 0; i < 16; i++) tacc[i] = K::RB ? 0 : sp->l2n_ci[fcol];
-#pragma unroll
-    for (int fi = 0; fi < FPW; fi++) {
-      const int f = wave * FPW + fi;
-      const int8_t* pb = (fi_c == fi) ? smem_y1 + f * K::Y1ROW + (32 / K::P) * (32 * K::MT + b)
-                                      : zero + 48 * h - l2_boff<K>(0, h);  // reads zeros
-#pragma unroll
-      for (int s = 0; s < 3; s++)
-        tacc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, h)), tacc, 0, 0, 0);
-    }
-    const bool valid = cvalid;
-    const int fc = fcol;
-    const unsigned w = K::RB ? l2_out(tacc, sp->l2_thr[fc], sp->l2_off[fc], sp->l2_r[fc])
-                             : l2n_out(tacc, sp->l2n_r[fc], sp->l2n_c[fc]);
-    const int u0 = 4 * (32 * K::MT + b) + 2 * h;
-    if (valid && u0 < K::T8) {
-      int8_t* dst = smem_y2 + fc * K::Y2ROW + 8 + u0;
-      if (u0 + 1 < K::T8) *(unsigned short*)dst = (unsigned short)w;
-      else *dst = (int8_t)w;
-    }
+#endif
+#ifndef MIB_TAIL_FIRST
+    const v4i tacc = layer2_tail_mfma<K>(smem_y1, zero, sp, wave, lane);
+#endif
+    layer2_tail_out<K>(tacc, smem_y2, sp, wave, lane);
   }
 }
 
@@ -366,16 +461,17 @@ template <class K>
 __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, const SmallParams* sp,
                                        const Regs<K>& R, int wave, int lane) {
   const int col = lane & 15, g = lane >> 4;
-  const float r3 = sp->l3_r;
+  const float r3 = sp->l3_r, c3 = sp->l3_c;
   unsigned w[FPW];
 #pragma unroll
   for (int fi = 0; fi < FPW; fi++) {
     const int f = wave * FPW + fi;
     const long bv = *(const long*)(smem_y2 + f * K::Y2ROW + 16 * col + 8 * g);
-    v4i acc = {0, 0, 0, 0};
+    // C-init = float magic: acc bits = 1.5 * 2^23 + dot as f32, fma(bits, r, c) == RN(dot * r)
+    v4i acc = {FMAGIC_I, FMAGIC_I, FMAGIC_I, FMAGIC_I};
     acc = __builtin_amdgcn_mfma_i32_16x16x32_i8(R.a3[fi], bv, acc, 0, 0, 0);
-    const f2 q01 = (f2){(float)acc[0], (float)acc[1]} * (f2){r3, r3};
-    const f2 q23 = (f2){(float)acc[2], (float)acc[3]} * (f2){r3, r3};
+    const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(acc[0]), __int_as_float(acc[1])}, (f2){r3, r3}, (f2){c3, c3});
+    const f2 q23 = __builtin_elementwise_fma((f2){__int_as_float(acc[2]), __int_as_float(acc[3])}, (f2){r3, r3}, (f2){c3, c3});
     w[fi] = sat8x4((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
   }
   // interleave the two filters: pair i = bytes (f0[i], f1[i])
@@ -396,26 +492,24 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
 }
 
 // ---- layer 4 ---------------------------------------------------------------------------------
-// One wave.  MFMA t covers samples 64t .. 64t+63: A row i (lane (i, h)) = y3t[64t + 32h + n(i)] in
+// Part t (one wave, one MFMA) covers samples 64t .. 64t+63: A row i (lane (i, h)) = y3t[64t + 32h + n(i)] in
 // K-slots 16h..16h+15; B is block diagonal (columns c < 16: channel c on slots 0..15, columns
 // c >= 16: channel c-16 on slots 16..31), so column c of D = channel c & 15 of time block c >> 4.
 // Rows n(i) permuted so lane (c, h) register r = time 16h + r of that block: two pool-8 windows.
 template <class K>
-__device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, const SmallParams* sp, int lane) {
+__device__ __forceinline__ void layer4_part(const int8_t* smem_y3, int8_t* smem_y4, const SmallParams* sp, int t,
+                                            int lane) {
   const int i = lane & 31, h = lane >> 5, k = i & 15;
   const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
   const v4i bw = sp->l4_bfrag[lane];
   const int thr = sp->l4_thr[k], off = sp->l4_off[k];
   const float r4 = sp->l4_r[k];
-  v4i a[K::NT4];
-#pragma unroll
-  for (int t = 0; t < K::NT4; t++) a[t] = *(const v4i*)(smem_y3 + (64 * t + 32 * h + n) * K::Y3S);  // unaligned (4 B)
-#pragma unroll
-  for (int t = 0; t < K::NT4; t++) {
+  const v4i a = *(const v4i*)(smem_y3 + (64 * t + 32 * h + n) * K::Y3S);  // unaligned (4 B)
+  {
     v16i acc;
 #pragma unroll
     for (int j = 0; j < 16; j++) acc[j] = K::RB ? 0 : sp->l4n_ci[k];  // plain branch: C-init
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[t], bw, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bw, acc, 0, 0, 0);
     unsigned w;
     if constexpr (K::RB) {
       const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
@@ -470,8 +564,10 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
   return z0 | (z1 << 8) | (z2 << 16) | (z3 << 24);
 }
 
-// Diagnostics only (tools/probe.hip builds): MIB_DIAG_NOBAR drops the in-loop barriers (wrong
-// results, timing insight), MIB_DIAG_SAME_TRIAL makes every trial read trial 0 (L2-resident).
+// Diagnostics only (tools/probe.hip and tools/ab.py builds; all give wrong results, for timing
+// insight): MIB_DIAG_NOBAR drops the in-loop barriers, MIB_DIAG_SAME_TRIAL makes every trial read
+// trial 0 (L2-resident), MIB_DIAG_NOL1RQ / NOPOOL / NOTAIL / NOL2 / NOL3 / NOL45 skip the
+// layer-1 requant, the layer-2 pooling, the layer-2 tail tile, layer 2, layer 3, layers 4-5.
 #ifdef MIB_DIAG_NOBAR
 #define MIB_LOOP_BARRIER() ((void)0)
 #else
@@ -496,6 +592,11 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   if ((int)blockIdx.x < B) prefetch_l1<K>(x + (size_t)blockIdx.x * K::XTRIAL, R, wave, lane);
   __syncthreads();
   MIB_STAMP_INIT
+  // Per trial two barriers: A after layer 1 (layer 2 of a filter reads all waves' layer-1
+  // output), B after layer 3 (layer 4 reads all filters).  Layers 2 and 3 of a filter run on the
+  // wave that owns it, with no barrier between.  After B the last wave runs layers 4 and 5 while
+  // the others start the next trial's layer 1: the next trial's layers 1-2 touch neither y3t
+  // nor y4, and its layer 3 comes after the next A, which the last wave reaches only when done.
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const int bn = b + gridDim.x;
     const int8_t* xt = x + MIB_TRIAL_OFF(b);
@@ -506,21 +607,31 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     asm volatile("" : "+v"(ln));
     MIB_STAMP(5)
     layer1<K>(xt, xn, smem + K::OFF_Y1, R, wave, lane);
-    MIB_LOOP_BARRIER();
+    MIB_LOOP_BARRIER();  // A
     MIB_STAMP(0)
+#ifndef MIB_DIAG_NOL2
     layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, smem + K::OFF_ZERO, sp, R, wave, ln);
-    MIB_LOOP_BARRIER();
+#endif
+    // layer 3 of filter f reads only y2 row f, which this wave wrote
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     MIB_STAMP(1)
+#ifndef MIB_DIAG_NOL3
     layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, wave, ln);
-    MIB_LOOP_BARRIER();
+#endif
+    MIB_LOOP_BARRIER();  // B
     MIB_STAMP(2)
-    // layers 4 and 5 on the last wave (no barrier: the next trial's layers 1-2 touch neither
-    // y3t nor y4, and the next layer 3 waits at two barriers this wave also passes)
     if (wave == NWAVES - 1) {
-      layer4<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, ln);
+#ifdef MIB_DIAG_NOL45
+      if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = *(const unsigned*)(smem + K::OFF_Y3 + 4 * (b & 15));
+#else
+#pragma unroll
+      for (int t = 0; t < K::NT4; t++) layer4_part<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, t, ln);
       MIB_STAMP(3)
       const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, ln);
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = z;
+#endif
     }
     MIB_STAMP(4)
   }
@@ -581,7 +692,8 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
   } else if (stage == 4) {  // [T8][F2] -> [F2][T64_ALIGN]
     for (int i = tid; i < K::Y3ROWS * F2; i += NTHREADS) y3[(i / F2) * K::Y3S + (i % F2)] = i < K::T8 * F2 ? in[i] : 0;
     __syncthreads();
-    if (wave == 0) layer4<K>(y3, y4, sp, lane);
+    if (wave == 0)
+      for (int t = 0; t < K::NT4; t++) layer4_part<K>(y3, y4, sp, t, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T64_AL; i += NTHREADS) {
       const int k = i / T64_AL, v = i - k * T64_AL;

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -255,6 +256,20 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         }
         std::memcpy(&dp.l2_afrag[f][s][lane], bytes, 16);
       }
+    // tail band for MFMA 16x16x64: lane (m, g), K-step s holds slots 64 s + 16 g + jj; slot ->
+    // window position q as the device reads B (P == 2: plane g >> 1, plane byte 32 s + 16 (g & 1)
+    // + jj); row m = output shift, tap q - m - 1
+    for (int s = 0; s < 2; s++)
+      for (int lane = 0; lane < 64; lane++) {
+        const int m = lane & 15, g = lane >> 4;
+        int8_t bytes[16];
+        for (int jj = 0; jj < 16; jj++) {
+          const int q = P == 2 ? 2 * (32 * s + 16 * (g & 1) + jj) + (g >> 1) : 64 * s + 16 * g + jj;
+          const int idx = q - m - 1;
+          bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
+        }
+        std::memcpy(&dp.l2t_afrag[f][s][lane], bytes, 16);
+      }
     dp.l2_thr[f] = -(hp.l2_offset[f] >> 3);
     dp.l2_off[f] = hp.l2_offset[f];
     if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f])) return NET_ERR_RANGE;
@@ -282,7 +297,8 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
       std::memcpy(&dp.l3_afrag[f][lane], bytes, 8);
     }
   }
-  if (!choose_reciprocal(hp.l3_factor, &sp.l3_r)) return NET_ERR_RANGE;
+  // |layer-3 accumulator| <= 16 * 128 * 128 < 2^22: magic C-init form
+  if (!choose_reciprocal(hp.l3_factor, &sp.l3_r, &sp.l3_c)) return NET_ERR_RANGE;
   // layer 4: B operand of MFMA 32x32x32 = W4^T, block diagonal: lane (column k, half h) holds
   // K-slots 16h..16h+15; columns 0..15 carry output channels 0..15 on slots 0..15 and columns
   // 16..31 repeat them on slots 16..31 (a second 32-sample time block rides in the other K half).
@@ -335,7 +351,6 @@ struct DeviceState {
   int8_t* d_out = nullptr;
   size_t scratch = 0;
   int cus = 0;
-  int blocks_per_cu = 0;
 };
 
 std::mutex g_mu;
@@ -404,13 +419,15 @@ int ensure_scratch(DeviceState& ds, size_t bytes) {
 template <class K>
 int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y, size_t B,
                      hipStream_t st, int32_t* info) {
-  if (ds.blocks_per_cu == 0) {
-    int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, wg::k_forward<K>, wg::NTHREADS, 0) != hipSuccess || nb < 1)
-      nb = 1;
-    ds.blocks_per_cu = nb;
+  static std::atomic<int> bpc{0};  // per kernel instantiation (LDS and registers differ)
+  int blocks_per_cu = bpc.load();
+  if (blocks_per_cu == 0) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, wg::k_forward<K>, wg::NTHREADS, 0) != hipSuccess ||
+        blocks_per_cu < 1)
+      blocks_per_cu = 1;
+    bpc.store(blocks_per_cu);
   }
-  const size_t cap = (size_t)ds.cus * (size_t)ds.blocks_per_cu;
+  const size_t cap = (size_t)ds.cus * (size_t)blocks_per_cu;
   const int grid = (int)(B < cap ? B : cap);
   if (info) { info[0] = grid; info[1] = wg::NTHREADS; info[2] = K::LDS; return NET_OK; }
   if (B == 0) return NET_OK;

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Same-box A/B timing of library builds (diagnostic; not part of the product).
+
+Loads each given libmibminet variant (tools/build_diag.sh builds them with -D flags), loads the
+same synthetic parameter blob into each, and times net_model_compute_batch_async on one resident
+batch, interleaving the variants round by round so clock drift hits all of them alike.
+
+    python tools/ab.py [--cfg b22|c64] [--B 65536] [--iters 20] [--rounds 5] lib1.so lib2.so ...
+"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "mi-bminet_amd"))
+from mibminet.params import ParamSet  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cfg", default="b22")
+    ap.add_argument("--B", type=int, default=65536)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("libs", nargs="+")
+    a = ap.parse_args()
+    C, T = {"b22": (22, 1125), "c64": (64, 1000)}[a.cfg]
+    blob = ParamSet.synthetic(seed=1, C=C, T=T).to_blob()
+    libs = []
+    for p in a.libs:
+        L = ctypes.CDLL(os.path.abspath(p), mode=ctypes.RTLD_LOCAL)
+        L.net_params_load.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.net_trial_stride.restype = ctypes.c_size_t
+        L.net_model_compute_batch_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                    ctypes.c_int, ctypes.c_void_p]
+        rc = L.net_params_load(blob, len(blob))
+        assert rc == 0, (p, rc)
+        libs.append(L)
+    stride = libs[0].net_trial_stride()
+    x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0")
+    y = torch.empty((a.B, 4), dtype=torch.int8, device="cuda:0")
+    st = torch.cuda.current_stream()
+    outs = []
+    for L in libs:
+        y.zero_()
+        assert L.net_model_compute_batch_async(x.data_ptr(), y.data_ptr(), a.B, 0, st.cuda_stream) == 0
+        outs.append(y.clone())
+    for p, o in zip(a.libs, outs):
+        same = bool(torch.equal(o, outs[0]))
+        print(f"{os.path.basename(p):28s} output {'==' if same else '!='} first library's", flush=True)
+    times = {p: [] for p in a.libs}
+    for r in range(a.rounds):
+        for p, L in zip(a.libs, libs):
+            for _ in range(2):
+                L.net_model_compute_batch_async(x.data_ptr(), y.data_ptr(), a.B, 0, st.cuda_stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.iters):
+                rc = L.net_model_compute_batch_async(x.data_ptr(), y.data_ptr(), a.B, 0, st.cuda_stream)
+            e1.record(st)
+            e1.synchronize()
+            assert rc == 0, (p, rc)
+            times[p].append(e0.elapsed_time(e1) / a.iters)
+        print(f"round {r}: " + "  ".join(f"{os.path.basename(p)}={times[p][-1]:.4f}" for p in a.libs), flush=True)
+    base = statistics.median(times[a.libs[0]])
+    for p in a.libs:
+        m = statistics.median(times[p])
+        print(f"{os.path.basename(p):28s} median {m:.4f} ms  ({(m / base - 1) * 100:+.1f}% vs first)")
+
+
+if __name__ == "__main__":
+    main()
