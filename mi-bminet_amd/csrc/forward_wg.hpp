@@ -102,8 +102,7 @@ struct Cfg {
   static constexpr int OFF_Y2 = OFF_Y1 + F2 * Y1ROW;
   static constexpr int OFF_Y3 = OFF_Y2 + align16(F2 * Y2ROW) + 256;  // layer-3 reads may run 256 B past
   static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S);
-  static constexpr int OFF_ZERO = OFF_Y4 + align16(64 * N5L);
-  static constexpr int OFF_SP = OFF_ZERO + 128;
+  static constexpr int OFF_SP = OFF_Y4 + align16(64 * N5L);
   static constexpr int OFF_L2T = align16(OFF_SP + (int)sizeof(SmallParams));  // tail band fragments
   static constexpr int LDS = OFF_L2T + (TB > 0 ? F2 * 2 * 64 * 16 : 0);
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
@@ -112,7 +111,6 @@ struct Cfg {
   static_assert(16 * N5L <= ND5_MAX, "layer-5 input too long");
   static_assert(MT >= 1, "at least one full layer-2 tile");
   static_assert(FPW * TC <= 16, "tail columns of a wave fit one 16-column tile");
-  static_assert(OFF_ZERO >= F2 * Y1ROW, "zero-row addressing stays non-negative");
 };
 
 // byte offset of layer-1 output (filter f, sample t) inside the LDS rows
@@ -341,40 +339,51 @@ __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, fl
   return sat8x2((int)q[0], (int)q[1]);
 }
 
-// Layer-2 tail: outputs 1024 MT + 16 bq + m (m < 16) of the wave's filters on MFMA
-// i32_16x16x64_i8.  Column col = TC fi + bq; A = the filter's 16-shift band (LDS, [f][s][lane]);
-// B lane (col, g), K-step s = 16 bytes of the column's 128-position window (P == 2: plane g >> 1,
-// plane bytes 32 s + 16 (g & 1) .. +15, 8-byte aligned).  Slots past window position 79 meet zero
+// Layer-2 tail: outputs 1024 MT + 16 bq + m (m < 16) of the wave's filters.  Column col =
+// TC fi + bq belongs to filter fi.  Per filter two MFMA i32_16x16x64_i8 (K-steps s = 0, 1: window
+// positions 0..127; taps reach position 79), A = the filter's 16-shift band (LDS).  B = every
+// lane's own column, read once and multiplied by both filters' bands; each lane keeps the
+// accumulator of its own filter.  P == 2: lane (col, g), step s reads parity plane g >> 1, plane
+// bytes 32 s + 16 (g & 1) .. +15 of the column's window.  Slots past position 79 meet zero
 // weights, so the window may run into the next plane / row.  D lane (col, g) holds shifts
 // 4g .. 4g+3: half of pool window g >> 1; lanes g and g ^ 1 are rows 2k, 2k+1 of the wave and
 // meet by v_permlane16_swap.
 template <class K>
-__device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const int8_t* zero, const SmallParams* sp,
-                                                int wave, int lane) {
+__device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const SmallParams* sp, int wave, int lane) {
   const int col = lane & 15, g = lane >> 4;
   const int fi_c = col / K::TC, bq = col - fi_c * K::TC;
   const int fcol = wave * FPW + (fi_c < FPW ? fi_c : 0);
   const v4i* tA = (const v4i*)(smem_y1 - K::OFF_Y1 + K::OFF_L2T);
   constexpr int SOFF = K::P == 2 ? 32 : 64;  // B byte offset of K-step 1
-  const int boff = (K::P == 2) ? (g >> 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (g & 1)
-                               : 1024 * K::MT + 16 * bq + 16 * g;
-  v4i tacc;
+  const int8_t* pb = smem_y1 + fcol * K::Y1ROW +
+                     ((K::P == 2) ? (g >> 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (g & 1)
+                                  : 1024 * K::MT + 16 * bq + 16 * g);
+  v4i bv[2];
 #pragma unroll
-  for (int i = 0; i < 4; i++) tacc[i] = K::RB ? 0 : sp->l2n_ci[fcol];
+  for (int s = 0; s < 2; s++) {
+    const long* q = (const long*)(pb + SOFF * s);  // 8-byte aligned
+    const long lo = q[0], hi = q[1];
+    bv[s][0] = (int)lo; bv[s][1] = (int)(lo >> 32); bv[s][2] = (int)hi; bv[s][3] = (int)(hi >> 32);
+  }
+  v4i acc[FPW], a[FPW][2];
 #pragma unroll
   for (int fi = 0; fi < FPW; fi++) {
     const int f = wave * FPW + fi;
-    const int8_t* pb = (fi_c == fi) ? smem_y1 + f * K::Y1ROW + boff : zero + 16 * g;
+    const int ci = K::RB ? 0 : sp->l2n_ci[f];
+    acc[fi] = (v4i){ci, ci, ci, ci};
 #pragma unroll
     for (int s = 0; s < 2; s++) {
-      const long* q = (const long*)(pb + SOFF * s);
-      const long lo = q[0], hi = q[1];
-      v4i bv;
-      bv[0] = (int)lo; bv[1] = (int)(lo >> 32); bv[2] = (int)hi; bv[3] = (int)(hi >> 32);
-      tacc = __builtin_amdgcn_mfma_i32_16x16x64_i8(tA[(2 * f + s) * 64 + lane], bv, tacc, 0, 0, 0);
+      a[fi][s] = tA[(2 * f + s) * 64 + lane];
+      acc[fi] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[fi][s], bv[s], acc[fi], 0, 0, 0);
     }
   }
-  return tacc;
+  // Operands stay live until the results are ready.  A version mixing 16x16x64 and 16x16x32
+  // steps in these chains gave wrong tail sums on gfx950 for some register allocations, while
+  // the same sequences in isolation (tools/mfma_hazard*.hip) were correct; see DESIGN.md.
+  asm volatile("" : "+v"(acc[0]), "+v"(acc[1]) : "v"(a[0][0]), "v"(a[0][1]), "v"(a[1][0]), "v"(a[1][1]), "v"(bv[0]),
+               "v"(bv[1]));
+  static_assert(FPW == 2, "two accumulators");
+  return fi_c == 0 ? acc[0] : acc[1];
 }
 
 template <class K>
@@ -407,14 +416,8 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
 // Layer 2: y1 rows -> y2 rows (LDS, position 8 + u).  Full tiles of the wave's filters, then the
 // tail (layer2_tail).
 template <class K>
-__device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, const int8_t* zero,
-                                       const SmallParams* sp, const Regs<K>& R, int wave, int lane) {
+__device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, const SmallParams* sp, const Regs<K>& R, int wave, int lane) {
   const int c = lane & 31, h = lane >> 5;
-#if !defined(MIB_DIAG_NOTAIL) && defined(MIB_TAIL_FIRST)
-  // the tail's MFMAs first: their latency hides behind the full tiles
-  v4i tacc;
-  if constexpr (K::TB > 0) tacc = layer2_tail_mfma<K>(smem_y1, zero, sp, wave, lane);
-#endif
 #pragma unroll
   for (int mt = 0; mt < K::MT; mt++)
 #pragma unroll
@@ -444,9 +447,7 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 #else
   if constexpr (K::TB > 0) {
 #endif
-#ifndef MIB_TAIL_FIRST
-    const v4i tacc = layer2_tail_mfma<K>(smem_y1, zero, sp, wave, lane);
-#endif
+    const v4i tacc = layer2_tail_mfma<K>(smem_y1, sp, wave, lane);
     layer2_tail_out<K>(tacc, smem_y2, sp, wave, lane);
   }
 }
@@ -610,12 +611,16 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     MIB_LOOP_BARRIER();  // A
     MIB_STAMP(0)
 #ifndef MIB_DIAG_NOL2
-    layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, smem + K::OFF_ZERO, sp, R, wave, ln);
+    layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, wave, ln);
 #endif
     // layer 3 of filter f reads only y2 row f, which this wave wrote
+#ifdef MIB_DIAG_L23BAR
+    __syncthreads();
+#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
     MIB_STAMP(1)
 #ifndef MIB_DIAG_NOL3
     layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, wave, ln);
@@ -671,7 +676,7 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
       y1[y1_index<K>(f, t)] = in[f * T_AL + t];
     }
     __syncthreads();
-    layer2<K>(y1, y2, smem + K::OFF_ZERO, sp, R, wave, lane);
+    layer2<K>(y1, y2, sp, R, wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T8_AL; i += NTHREADS) {
       const int f = i / T8_AL, u = i - f * T8_AL;
