@@ -91,17 +91,17 @@ struct Cfg {
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   static constexpr int Y2ROW = odd_dwords(cmax(T8 + 24, 16 * NB3 + 24));
   static constexpr int Y3ROWS = cmax(64 * NT4, T8);
-  // y3t rows are 20 bytes apart (16 filters + 4 pad): layer 3's 2-byte stores from 64 lanes
-  // (64 different rows) then hit 64 different banks; layer 4 reads a row with one unaligned
-  // ds_read_b128 (3 per trial)
-  static constexpr int Y3S = 20;
+  // y3t row u (16 filters) starts at byte 16 u + 4 (u >> 4) (y3_off): layer 3's 2-byte stores
+  // (one wave instruction covers rows 16 col + 4 g + i of 32 lanes) then hit 32 different banks;
+  // layer 4 reads a row with one (4-byte aligned) ds_read_b128, 2-way at most (3 per trial)
+  static constexpr int Y3S = 16;
   static constexpr int ND5 = (F2 * T64 + 3) / 4;        // layer-5 input dwords
   static constexpr int N5L = (ND5 + 15) / 16;           // layer-5 dwords per lane
   // LDS carve
   static constexpr int OFF_Y1 = 0;
   static constexpr int OFF_Y2 = OFF_Y1 + F2 * Y1ROW;
   static constexpr int OFF_Y3 = OFF_Y2 + align16(F2 * Y2ROW) + 256;  // layer-3 reads may run 256 B past
-  static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S);
+  static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S + 4 * (Y3ROWS >> 4));
   static constexpr int OFF_SP = OFF_Y4 + align16(64 * N5L);
   static constexpr int OFF_L2T = align16(OFF_SP + (int)sizeof(SmallParams));  // tail band fragments
   static constexpr int LDS = OFF_L2T + (TB > 0 ? F2 * 2 * 64 * 16 : 0);
@@ -118,6 +118,12 @@ template <class K>
 __device__ __forceinline__ int y1_index(int f, int t) {
   if constexpr (K::P == 2) return f * K::Y1ROW + (t & 1) * K::PLANE + ((t + 32) >> 1);
   else return f * K::Y1ROW + 32 + t;
+}
+
+// byte offset of y3t row u (see Cfg::Y3S)
+template <class K>
+__device__ __forceinline__ int y3_off(int u) {
+  return u * K::Y3S + 4 * (u >> 4);
 }
 
 // layer-2 B operand: byte offset (within a filter's rows, column block 0) of the 16-byte slice of
@@ -479,7 +485,7 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
   const unsigned p01 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u);  // f0[0] f1[0] f0[1] f1[1]
   const unsigned p23 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u);  // f0[2] f1[2] f0[3] f1[3]
   const int u = 16 * col + 4 * g;
-  int8_t* dst = smem_y3 + u * K::Y3S + FPW * wave;
+  int8_t* dst = smem_y3 + y3_off<K>(u) + FPW * wave;  // rows u .. u+3 share the skew
   if (u + 3 < K::T8) {
     *(unsigned short*)dst = (unsigned short)p01;
     *(unsigned short*)(dst + K::Y3S) = (unsigned short)(p01 >> 16);
@@ -505,7 +511,7 @@ __device__ __forceinline__ void layer4_part(const int8_t* smem_y3, int8_t* smem_
   const v4i bw = sp->l4_bfrag[lane];
   const int thr = sp->l4_thr[k], off = sp->l4_off[k];
   const float r4 = sp->l4_r[k];
-  const v4i a = *(const v4i*)(smem_y3 + (64 * t + 32 * h + n) * K::Y3S);  // unaligned (4 B)
+  const v4i a = *(const v4i*)(smem_y3 + y3_off<K>(64 * t + 32 * h + n));  // unaligned (4 B)
   {
     v16i acc;
 #pragma unroll
@@ -692,10 +698,10 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
     __syncthreads();
     for (int i = tid; i < F2 * T8_AL; i += NTHREADS) {
       const int f = i / T8_AL, u = i - f * T8_AL;
-      out[i] = u < K::T8 ? y3[u * K::Y3S + f] : 0;
+      out[i] = u < K::T8 ? y3[y3_off<K>(u) + f] : 0;
     }
   } else if (stage == 4) {  // [T8][F2] -> [F2][T64_ALIGN]
-    for (int i = tid; i < K::Y3ROWS * F2; i += NTHREADS) y3[(i / F2) * K::Y3S + (i % F2)] = i < K::T8 * F2 ? in[i] : 0;
+    for (int i = tid; i < K::Y3ROWS * F2; i += NTHREADS) y3[y3_off<K>(i / F2) + (i % F2)] = i < K::T8 * F2 ? in[i] : 0;
     __syncthreads();
     if (wave == 0)
       for (int t = 0; t < K::NT4; t++) layer4_part<K>(y3, y4, sp, t, lane);
