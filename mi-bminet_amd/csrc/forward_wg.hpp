@@ -103,7 +103,8 @@ struct Cfg {
   static constexpr int OFF_Y3 = OFF_Y2 + align16(F2 * Y2ROW) + 256;  // layer-3 reads may run 256 B past
   static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S + 4 * (Y3ROWS >> 4));
   static constexpr int OFF_SP = OFF_Y4 + align16(64 * N5L);
-  static constexpr int OFF_L2T = align16(OFF_SP + (int)sizeof(SmallParams));  // tail band fragments
+  static constexpr int OFF_LT = align16(OFF_SP + (int)sizeof(SmallParams));   // per-lane offsets
+  static constexpr int OFF_L2T = OFF_LT + 64 * 32;                            // tail band fragments
   static constexpr int LDS = OFF_L2T + (TB > 0 ? F2 * 2 * 64 * 16 : 0);
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
   static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
@@ -120,6 +121,20 @@ __device__ __forceinline__ int y1_index(int f, int t) {
   else return f * K::Y1ROW + 32 + t;
 }
 
+// Per-lane LDS offsets of layers 2 and 3 (wave-independent parts), built once per workgroup by
+// build_lane_tab and re-read every trial with two ds_read_b128: cheaper than recomputing them
+// from the lane id, and registers are too scarce to keep them live across the trial loop.
+struct LaneTab {
+  int l2b;  // full tile, B slice (filter 0, tile 0, K-step 0): (32 / P) c + l2_boff(0, h)
+  int l2y;  // full tile, y2 store (filter 0, tile 0): 8 + 4 c + 2 h
+  int tb;   // tail B window: fi_c * Y1ROW + window offset of (col, g)
+  int ty;   // tail y2 store: fi_c * Y2ROW + 8 + u, or -1 (lane stores nothing)
+  int tp;   // tail: filter slot fi_c of this lane's column (0 or 1)
+  int l3b;  // layer-3 B slice: 16 col + 8 g
+  int l3w;  // layer-3 store: y3_off(16 col + 4 g), or -1 (rows past T8)
+  int pad;
+};
+
 // byte offset of y3t row u (see Cfg::Y3S)
 template <class K>
 __device__ __forceinline__ int y3_off(int u) {
@@ -134,6 +149,32 @@ template <class K>
 __device__ __forceinline__ int l2_boff(int s, int h) {
   if constexpr (K::P == 2) return h * K::PLANE + 16 * s;
   else return 32 * s + 16 * h;
+}
+
+template <class K>
+__device__ __forceinline__ LaneTab build_lane_tab(int lane) {
+  LaneTab T;
+  {
+    const int c = lane & 31, h = lane >> 5;
+    T.l2b = (32 / K::P) * c + l2_boff<K>(0, h);
+    T.l2y = 8 + 4 * c + 2 * h;
+  }
+  {
+    const int col = lane & 15, g = lane >> 4;
+    const int fi_c = K::TC > 0 ? col / cmax(K::TC, 1) : 0, bq = col - fi_c * K::TC;
+    const bool cvalid = fi_c < FPW;
+    const int fs = cvalid ? fi_c : 0;
+    T.tb = fs * K::Y1ROW + ((K::P == 2) ? (g >> 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (g & 1)
+                                         : 1024 * K::MT + 16 * bq + 16 * g);
+    const int u = 128 * K::MT + 2 * bq + (g >> 1);
+    T.ty = (cvalid && !(g & 1) && u < K::T8) ? fs * K::Y2ROW + 8 + u : -1;
+    T.tp = fs;
+    T.l3b = 16 * col + 8 * g;
+    const int u3 = 16 * col + 4 * g;
+    T.l3w = u3 < K::T8 ? y3_off<K>(u3) : -1;
+  }
+  T.pad = 0;
+  return T;
 }
 
 // Per-lane register state that lives across the trial loop.
@@ -238,6 +279,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   const v4i* src = (const v4i*)&prm->sp;
   v4i* dst = (v4i*)(smem + K::OFF_SP);
   for (int i = tid; i < (int)(sizeof(SmallParams) / 16); i += NTHREADS) dst[i] = src[i];
+  if (tid < 64) ((LaneTab*)(smem + K::OFF_LT))[tid] = build_lane_tab<K>(tid);
   if constexpr (K::TB > 0) {
     const v4i* t = &prm->l2t_afrag[0][0][0];
     v4i* d = (v4i*)(smem + K::OFF_L2T);
@@ -355,15 +397,11 @@ __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, fl
 // 4g .. 4g+3: half of pool window g >> 1; lanes g and g ^ 1 are rows 2k, 2k+1 of the wave and
 // meet by v_permlane16_swap.
 template <class K>
-__device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const SmallParams* sp, int wave, int lane) {
-  const int col = lane & 15, g = lane >> 4;
-  const int fi_c = col / K::TC, bq = col - fi_c * K::TC;
-  const int fcol = wave * FPW + (fi_c < FPW ? fi_c : 0);
+__device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const SmallParams* sp, const LaneTab& T,
+                                                int wave, int lane) {
   const v4i* tA = (const v4i*)(smem_y1 - K::OFF_Y1 + K::OFF_L2T);
   constexpr int SOFF = K::P == 2 ? 32 : 64;  // B byte offset of K-step 1
-  const int8_t* pb = smem_y1 + fcol * K::Y1ROW +
-                     ((K::P == 2) ? (g >> 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (g & 1)
-                                  : 1024 * K::MT + 16 * bq + 16 * g);
+  const int8_t* pb = smem_y1 + wave * FPW * K::Y1ROW + T.tb;
   v4i bv[2];
 #pragma unroll
   for (int s = 0; s < 2; s++) {
@@ -389,16 +427,13 @@ __device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const Sma
   asm volatile("" : "+v"(acc[0]), "+v"(acc[1]) : "v"(a[0][0]), "v"(a[0][1]), "v"(a[1][0]), "v"(a[1][1]), "v"(bv[0]),
                "v"(bv[1]));
   static_assert(FPW == 2, "two accumulators");
-  return fi_c == 0 ? acc[0] : acc[1];
+  return T.tp == 0 ? acc[0] : acc[1];
 }
 
 template <class K>
-__device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2, const SmallParams* sp, int wave,
-                                                int lane) {
-  const int col = lane & 15, g = lane >> 4;
-  const int fi_c = col / K::TC, bq = col - fi_c * K::TC;
-  const bool cvalid = fi_c < FPW;
-  const int fcol = wave * FPW + (cvalid ? fi_c : 0);
+__device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2, const SmallParams* sp,
+                                                const LaneTab& T, int wave) {
+  const int fcol = wave * FPW + T.tp;
   int part;
   if constexpr (K::RB) {
     const int thr = sp->l2_thr[fcol];
@@ -415,27 +450,27 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
   int y;
   if constexpr (K::RB) y = rq(tot + sp->l2_off[fcol], sp->l2_r[fcol]);
   else y = tot >> 3;
-  const int u = 128 * K::MT + 2 * bq + (g >> 1);
-  if (cvalid && !(g & 1) && u < K::T8) smem_y2[fcol * K::Y2ROW + 8 + u] = (int8_t)y;
+  if (T.ty >= 0) smem_y2[wave * FPW * K::Y2ROW + T.ty] = (int8_t)y;
 }
 
 // Layer 2: y1 rows -> y2 rows (LDS, position 8 + u).  Full tiles of the wave's filters, then the
 // tail (layer2_tail).
 template <class K>
-__device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, const SmallParams* sp, const Regs<K>& R, int wave, int lane) {
+__device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, const SmallParams* sp,
+                                       const Regs<K>& R, const LaneTab& T, int wave, int lane) {
   const int c = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int mt = 0; mt < K::MT; mt++)
 #pragma unroll
     for (int fi = 0; fi < FPW; fi++) {
       const int f = wave * FPW + fi;
-      const int8_t* pb = smem_y1 + f * K::Y1ROW + (32 / K::P) * (32 * mt + c);
+      const int8_t* pb = smem_y1 + f * K::Y1ROW + (32 / K::P) * 32 * mt + T.l2b - l2_boff<K>(0, 0);
       v16i acc;
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = K::RB ? 0 : R.thr2[fi];  // plain branch: C-init
 #pragma unroll
       for (int s = 0; s < 3; s++)
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, h)), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, 0)), acc, 0, 0, 0);
       // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
 #ifdef MIB_DIAG_NOPOOL
       const unsigned w = acc[0] ^ acc[5] ^ acc[10] ^ acc[15];
@@ -443,18 +478,22 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
       const unsigned w = K::RB ? l2_out(acc, R.thr2[fi], R.off2[fi], R.r2[fi])
                                : l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
 #endif
-      const int u0 = 4 * (32 * mt + c) + 2 * h;
-      int8_t* dst = smem_y2 + f * K::Y2ROW + 8 + u0;
-      if (128 * (mt + 1) <= K::T8 || u0 + 1 < K::T8) *(unsigned short*)dst = (unsigned short)w;
-      else if (u0 < K::T8) *dst = (int8_t)w;
+      int8_t* dst = smem_y2 + f * K::Y2ROW + 128 * mt + T.l2y;
+      if (128 * (mt + 1) <= K::T8) {
+        *(unsigned short*)dst = (unsigned short)w;
+      } else {
+        const int u0 = 4 * (32 * mt + c) + 2 * h;
+        if (u0 + 1 < K::T8) *(unsigned short*)dst = (unsigned short)w;
+        else if (u0 < K::T8) *dst = (int8_t)w;
+      }
     }
 #ifdef MIB_DIAG_NOTAIL
   if constexpr (false) {
 #else
   if constexpr (K::TB > 0) {
 #endif
-    const v4i tacc = layer2_tail_mfma<K>(smem_y1, sp, wave, lane);
-    layer2_tail_out<K>(tacc, smem_y2, sp, wave, lane);
+    const v4i tacc = layer2_tail_mfma<K>(smem_y1, sp, T, wave, lane);
+    layer2_tail_out<K>(tacc, smem_y2, sp, T, wave);
   }
 }
 
@@ -466,14 +505,13 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 // bytes of one output are adjacent in y3t[u][f] and go out as one 2-byte store.
 template <class K>
 __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, const SmallParams* sp,
-                                       const Regs<K>& R, int wave, int lane) {
-  const int col = lane & 15, g = lane >> 4;
+                                       const Regs<K>& R, const LaneTab& T, int wave) {
   const float r3 = sp->l3_r, c3 = sp->l3_c;
   unsigned w[FPW];
 #pragma unroll
   for (int fi = 0; fi < FPW; fi++) {
     const int f = wave * FPW + fi;
-    const long bv = *(const long*)(smem_y2 + f * K::Y2ROW + 16 * col + 8 * g);
+    const long bv = *(const long*)(smem_y2 + f * K::Y2ROW + T.l3b);
     // C-init = float magic: acc bits = 1.5 * 2^23 + dot as f32, fma(bits, r, c) == RN(dot * r)
     v4i acc = {FMAGIC_I, FMAGIC_I, FMAGIC_I, FMAGIC_I};
     acc = __builtin_amdgcn_mfma_i32_16x16x32_i8(R.a3[fi], bv, acc, 0, 0, 0);
@@ -484,17 +522,14 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
   // interleave the two filters: pair i = bytes (f0[i], f1[i])
   const unsigned p01 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u);  // f0[0] f1[0] f0[1] f1[1]
   const unsigned p23 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u);  // f0[2] f1[2] f0[3] f1[3]
-  const int u = 16 * col + 4 * g;
-  int8_t* dst = smem_y3 + y3_off<K>(u) + FPW * wave;  // rows u .. u+3 share the skew
-  if (u + 3 < K::T8) {
+  // rows u .. u+3 (u = 16 col + 4 g) share the skew.  Rows T8 .. u+3 of the last block are
+  // written too: layer 4 multiplies rows >= T8 only into its discarded outputs (v >= T64).
+  if (T.l3w >= 0) {
+    int8_t* dst = smem_y3 + T.l3w + FPW * wave;
     *(unsigned short*)dst = (unsigned short)p01;
     *(unsigned short*)(dst + K::Y3S) = (unsigned short)(p01 >> 16);
     *(unsigned short*)(dst + 2 * K::Y3S) = (unsigned short)p23;
     *(unsigned short*)(dst + 3 * K::Y3S) = (unsigned short)(p23 >> 16);
-  } else {
-    if (u < K::T8) *(unsigned short*)dst = (unsigned short)p01;
-    if (u + 1 < K::T8) *(unsigned short*)(dst + K::Y3S) = (unsigned short)(p01 >> 16);
-    if (u + 2 < K::T8) *(unsigned short*)(dst + 2 * K::Y3S) = (unsigned short)p23;
   }
 }
 
@@ -616,8 +651,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     layer1<K>(xt, xn, smem + K::OFF_Y1, R, wave, lane);
     MIB_LOOP_BARRIER();  // A
     MIB_STAMP(0)
+    const LaneTab T = ((const LaneTab*)(smem + K::OFF_LT))[ln];
 #ifndef MIB_DIAG_NOL2
-    layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, wave, ln);
+    layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, T, wave, ln);
 #endif
     // layer 3 of filter f reads only y2 row f, which this wave wrote
 #ifdef MIB_DIAG_L23BAR
@@ -629,7 +665,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
 #endif
     MIB_STAMP(1)
 #ifndef MIB_DIAG_NOL3
-    layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, wave, ln);
+    layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, T, wave);
 #endif
     MIB_LOOP_BARRIER();  // B
     MIB_STAMP(2)
@@ -682,7 +718,7 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
       y1[y1_index<K>(f, t)] = in[f * T_AL + t];
     }
     __syncthreads();
-    layer2<K>(y1, y2, sp, R, wave, lane);
+    layer2<K>(y1, y2, sp, R, ((const LaneTab*)(smem + K::OFF_LT))[lane], wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T8_AL; i += NTHREADS) {
       const int f = i / T8_AL, u = i - f * T8_AL;
@@ -694,7 +730,7 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
       y2[f * K::Y2ROW + 8 + u] = in[f * T8_AL + u];
     }
     __syncthreads();
-    layer3<K>(y2, y3, sp, R, wave, lane);
+    layer3<K>(y2, y3, sp, R, ((const LaneTab*)(smem + K::OFF_LT))[lane], wave);
     __syncthreads();
     for (int i = tid; i < F2 * T8_AL; i += NTHREADS) {
       const int f = i / T8_AL, u = i - f * T8_AL;
