@@ -38,8 +38,15 @@ constexpr int NWAVES = 8;             // waves per workgroup (one trial per work
 constexpr int FPW = F2 / NWAVES;      // layer-2 / layer-3 filters per wave
 constexpr int NTHREADS = 64 * NWAVES;
 constexpr int WPE = 4;                // waves per SIMD (two workgroups per CU)
-constexpr int PF_MAX = 9;             // layer-1 blocks per wave prefetched one trial ahead
+#ifndef MIB_PF_MAX
+#define MIB_PF_MAX 9
+#endif
+constexpr int PF_MAX = MIB_PF_MAX;    // layer-1 blocks per wave prefetched one trial ahead
 static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wave");
+// Wave priorities (s_setprio): the last wave's layers 4-5 are the longest dependency chain of the
+// layer-1 interval, so that wave issues first while on them; layer 1 (HBM fragments, next-trial
+// prefetch) goes ahead of the other workgroup's layers 2-3.  Same-box A/B: -4 %.
+constexpr int PRIO_L1 = 1, PRIO_L45 = 3;
 
 // Layer-1 work split.  The last wave also runs layers 4 and 5 (in the same barrier interval as
 // the next trial's layer 1), so it takes fewer layer-1 blocks: waves 0 .. NWAVES-2 get cm blocks
@@ -648,7 +655,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     int ln = lane;
     asm volatile("" : "+v"(ln));
     MIB_STAMP(5)
+    __builtin_amdgcn_s_setprio(PRIO_L1);
     layer1<K>(xt, xn, smem + K::OFF_Y1, R, wave, lane);
+    __builtin_amdgcn_s_setprio(0);
     MIB_LOOP_BARRIER();  // A
     MIB_STAMP(0)
     const LaneTab T = ((const LaneTab*)(smem + K::OFF_LT))[ln];
@@ -670,6 +679,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     MIB_LOOP_BARRIER();  // B
     MIB_STAMP(2)
     if (wave == NWAVES - 1) {
+      __builtin_amdgcn_s_setprio(PRIO_L45);
 #ifdef MIB_DIAG_NOL45
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = *(const unsigned*)(smem + K::OFF_Y3 + 4 * (b & 15));
 #else
@@ -679,6 +689,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
       const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, ln);
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = z;
 #endif
+      __builtin_amdgcn_s_setprio(0);
     }
     MIB_STAMP(4)
   }
