@@ -19,7 +19,7 @@ constexpr int F2 = 16;          // filters (F1 == F2, D == 1)
 constexpr int N_OUT = 4;        // classes
 constexpr int L2_TAPS = 64;
 constexpr int L3_TAPS = 16;
-constexpr int ND5_MAX = 96;     // dwords of the flattened layer-4 output (F2*T64 <= 384)
+constexpr int ND5_MAX = 96;     // dwords of the layer-4 output [F2][T64_ALIGN] (F2*T64_ALIGN <= 384)
 constexpr int FMAGIC_I = 0x4B400000;   // bit pattern of 1.5 * 2^23
 
 // Diagnostic phase stamps (tools/probe.hip builds with -DMIB_STAMPS; compiled out otherwise).
@@ -61,7 +61,7 @@ struct SmallParams {
   int l4n_ci[F2];
   float l4n_r[F2];
   float l4n_c[F2];
-  int l5_w[N_OUT][ND5_MAX];  // flattened [k][v] order, zero padded
+  int l5_w[N_OUT][ND5_MAX];  // [k][v] with row stride T64_ALIGN, zero padded
   int l5_b[N_OUT];
   float l3_r;
   float l5_r;

@@ -102,7 +102,9 @@ struct Cfg {
   // (one wave instruction covers rows 16 col + 4 g + i of 32 lanes) then hit 32 different banks;
   // layer 4 reads a row with one (4-byte aligned) ds_read_b128, 2-way at most (3 per trial)
   static constexpr int Y3S = 16;
-  static constexpr int ND5 = (F2 * T64 + 3) / 4;        // layer-5 input dwords
+  static constexpr int T64A = (T64 + 3) & ~3;           // y4 row stride (reference T64_ALIGN)
+  static constexpr bool L4PIPE = P == 2 && RB;          // layer-4 MFMA/pooling overlap (registers)
+  static constexpr int ND5 = F2 * T64A / 4;             // layer-5 input dwords
   static constexpr int N5L = (ND5 + 15) / 16;           // layer-5 dwords per lane
   // LDS carve
   static constexpr int OFF_Y1 = 0;
@@ -546,47 +548,75 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
 // c >= 16: channel c-16 on slots 16..31), so column c of D = channel c & 15 of time block c >> 4.
 // Rows n(i) permuted so lane (c, h) register r = time 16h + r of that block: two pool-8 windows.
 template <class K>
-__device__ __forceinline__ void layer4_part(const int8_t* smem_y3, int8_t* smem_y4, const SmallParams* sp, int t,
-                                            int lane) {
+__device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* sp, int k) {
+  if constexpr (K::RB) {
+    const int thr = sp->l4_thr[k], off = sp->l4_off[k];
+    const float r4 = sp->l4_r[k];
+    const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
+    return sat8x2((int)q[0], (int)q[1]);
+  } else {
+    // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
+    // sum of 8, >> 3, clip.  Elements are clamped to [0, 1024]: any element >= 1024 already
+    // saturates the result, and the reciprocal is verified exact up to there.
+    const float rn = sp->l4n_r[k], cn = sp->l4n_c[k];
+    int sm[2];
+#pragma unroll
+    for (int hw = 0; hw < 2; hw++) {
+      int e[8];
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const f2 q = __builtin_elementwise_fma((f2){__int_as_float(acc[8 * hw + j]), __int_as_float(acc[8 * hw + j + 1])},
+                                               (f2){rn, rn}, (f2){cn, cn});
+        e[j] = (int)__builtin_amdgcn_fmed3f(q[0], 0.0f, 1024.0f);
+        e[j + 1] = (int)__builtin_amdgcn_fmed3f(q[1], 0.0f, 1024.0f);
+      }
+      sm[hw] = min((((e[0] + e[1] + e[2]) + (e[3] + e[4]) + (e[5] + e[6])) + e[7]) >> 3, 127);
+    }
+    return (unsigned)sm[0] | ((unsigned)sm[1] << 8);
+  }
+}
+
+// Layer 4 on one wave.  MFMA t covers samples 64t .. 64t+63.  Output y4[k][v], row stride T64A;
+// the pad columns v = T64 .. T64A-1 receive don't-care values (layer 5's weights there are zero).
+// L4PIPE: software-pipelined by one part (the MFMA of part t+1 is issued before the pooling of
+// part t, two accumulators live); otherwise one part at a time.
+template <class K>
+__device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, const SmallParams* sp, int lane) {
   const int i = lane & 31, h = lane >> 5, k = i & 15;
   const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
   const v4i bw = sp->l4_bfrag[lane];
-  const int thr = sp->l4_thr[k], off = sp->l4_off[k];
-  const float r4 = sp->l4_r[k];
-  const v4i a = *(const v4i*)(smem_y3 + y3_off<K>(64 * t + 32 * h + n));  // unaligned (4 B)
-  {
-    v16i acc;
+  const int ci = K::RB ? 0 : sp->l4n_ci[k];  // plain branch: C-init
+  if constexpr (K::L4PIPE) {
+    v4i a[K::NT4];
 #pragma unroll
-    for (int j = 0; j < 16; j++) acc[j] = K::RB ? 0 : sp->l4n_ci[k];  // plain branch: C-init
-    acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bw, acc, 0, 0, 0);
-    unsigned w;
-    if constexpr (K::RB) {
-      const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
-      w = sat8x2((int)q[0], (int)q[1]);
-    } else {
-      // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
-      // sum of 8, >> 3, clip.  Elements are clamped to [0, 1024]: any element >= 1024 already
-      // saturates the result, and the reciprocal is verified exact up to there.
-      const float rn = sp->l4n_r[k], cn = sp->l4n_c[k];
-      int sm[2];
+    for (int t = 0; t < K::NT4; t++) a[t] = *(const v4i*)(smem_y3 + y3_off<K>(64 * t + 32 * h + n));  // unaligned (4 B)
+    v16i acc[2];
 #pragma unroll
-      for (int hw = 0; hw < 2; hw++) {
-        int e[8];
+    for (int j = 0; j < 16; j++) acc[0][j] = ci;
+    acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], bw, acc[0], 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const f2 q = __builtin_elementwise_fma((f2){__int_as_float(acc[8 * hw + j]), __int_as_float(acc[8 * hw + j + 1])},
-                                                 (f2){rn, rn}, (f2){cn, cn});
-          e[j] = (int)__builtin_amdgcn_fmed3f(q[0], 0.0f, 1024.0f);
-          e[j + 1] = (int)__builtin_amdgcn_fmed3f(q[1], 0.0f, 1024.0f);
-        }
-        sm[hw] = min((((e[0] + e[1] + e[2]) + (e[3] + e[4]) + (e[5] + e[6])) + e[7]) >> 3, 127);
+    for (int t = 0; t < K::NT4; t++) {
+      if (t + 1 < K::NT4) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) acc[(t + 1) & 1][j] = ci;
+        acc[(t + 1) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[t + 1 < K::NT4 ? t + 1 : 0], bw, acc[(t + 1) & 1], 0, 0, 0);
       }
-      w = (unsigned)sm[0] | ((unsigned)sm[1] << 8);
+      const unsigned w = l4_out<K>(acc[t & 1], sp, k);
+      const int v0 = 8 * t + 4 * (i >> 4) + 2 * h;  // even
+      if (v0 < K::T64A) *(unsigned short*)(smem_y4 + k * K::T64A + v0) = (unsigned short)w;
     }
-    const int v0 = 8 * t + 4 * (i >> 4) + 2 * h;
-    int8_t* dst = smem_y4 + k * K::T64 + v0;
-    if (v0 < K::T64) dst[0] = (int8_t)w;
-    if (v0 + 1 < K::T64) dst[1] = (int8_t)(w >> 8);
+  } else {
+#pragma unroll
+    for (int t = 0; t < K::NT4; t++) {
+      const v4i a = *(const v4i*)(smem_y3 + y3_off<K>(64 * t + 32 * h + n));  // unaligned (4 B)
+      v16i acc;
+#pragma unroll
+      for (int j = 0; j < 16; j++) acc[j] = ci;
+      acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bw, acc, 0, 0, 0);
+      const unsigned w = l4_out<K>(acc, sp, k);
+      const int v0 = 8 * t + 4 * (i >> 4) + 2 * h;  // even
+      if (v0 < K::T64A) *(unsigned short*)(smem_y4 + k * K::T64A + v0) = (unsigned short)w;
+    }
   }
 }
 
@@ -597,7 +627,7 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
   int part = 0;
 #pragma unroll
   for (int j = 0; j < K::N5L; j++) {
-    const int i = c + 16 * j;  // dwords past ND5 meet zero weights (l5_w is zero padded)
+    const int i = c + 16 * j;  // pad columns and dwords past ND5 meet zero weights
     part = __builtin_amdgcn_sdot4(*(const int*)(smem_y4 + 4 * i), sp->l5_w[n][i], part, false);
   }
   // inclusive prefix sum within each 16-lane DPP row: lane 15 of the row holds the total
@@ -683,8 +713,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
 #ifdef MIB_DIAG_NOL45
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = *(const unsigned*)(smem + K::OFF_Y3 + 4 * (b & 15));
 #else
-#pragma unroll
-      for (int t = 0; t < K::NT4; t++) layer4_part<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, t, ln);
+      layer4<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, ln);
       MIB_STAMP(3)
       const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, ln);
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = z;
@@ -751,16 +780,16 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
     for (int i = tid; i < K::Y3ROWS * F2; i += NTHREADS) y3[y3_off<K>(i / F2) + (i % F2)] = i < K::T8 * F2 ? in[i] : 0;
     __syncthreads();
     if (wave == 0)
-      for (int t = 0; t < K::NT4; t++) layer4_part<K>(y3, y4, sp, t, lane);
+      layer4<K>(y3, y4, sp, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T64_AL; i += NTHREADS) {
       const int k = i / T64_AL, v = i - k * T64_AL;
-      out[i] = v < K::T64 ? y4[k * K::T64 + v] : 0;
+      out[i] = v < K::T64 ? y4[k * K::T64A + v] : 0;
     }
   } else if (stage == 5) {  // [F2][T64_ALIGN] -> [N]
     for (int i = tid; i < 64 * K::N5L; i += NTHREADS) {
-      const int k = i / K::T64, v = i - k * K::T64;
-      y4[i] = (k < F2) ? in[k * T64_AL + v] : 0;
+      const int k = i / K::T64A, v = i - k * K::T64A;
+      y4[i] = (k < F2 && v < K::T64) ? in[k * T64_AL + v] : 0;
     }
     __syncthreads();
     if (wave == 0) {

@@ -314,11 +314,11 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     if (!choose_reciprocal(hp.l4_factor[k], &sp.l4_r[k])) return NET_ERR_RANGE;
   }
   const int T64 = d.T64(), T64A = d.T64_ALIGN();
-  if ((F2 * T64 + 3) / 4 > ND5_MAX) return NET_ERR_UNSUPPORTED;
+  if (F2 * T64A / 4 > ND5_MAX) return NET_ERR_UNSUPPORTED;
   for (int n = 0; n < N_OUT; n++) {
     int8_t* dst = (int8_t*)sp.l5_w[n];
     for (int k = 0; k < F2; k++)
-      for (int v = 0; v < T64; v++) dst[k * T64 + v] = hp.l5_weight[(size_t)n * F2 * T64A + k * T64A + v];
+      for (int v = 0; v < T64; v++) dst[k * T64A + v] = hp.l5_weight[(size_t)n * F2 * T64A + k * T64A + v];
     sp.l5_b[n] = hp.l5_bias[n];
   }
   if (!choose_reciprocal(hp.l5_factor, &sp.l5_r)) return NET_ERR_RANGE;
