@@ -24,18 +24,20 @@ constexpr int FMAGIC_I = 0x4B400000;   // bit pattern of 1.5 * 2^23
 
 // Diagnostic phase stamps (tools/probe.hip builds with -DMIB_STAMPS; compiled out otherwise).
 #ifdef MIB_STAMPS
-__device__ unsigned long long g_stamps[16];
+// g_stamps[8 s + i]: phase i cycles summed over flusher slot s (0: wave 0, 1: last wave);
+// [16] s_memtime total, [17] s_memrealtime total, [18] flushers
+__device__ unsigned long long g_stamps[24];
 #define MIB_STAMP_INIT unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
   unsigned long long _st_t = __builtin_amdgcn_s_memtime(); \
   const unsigned long long _st_t0 = _st_t, _st_r0 = __builtin_amdgcn_s_memrealtime();
 #define MIB_STAMP(i) { const unsigned long long _t = __builtin_amdgcn_s_memtime(); _st_acc[i] += _t - _st_t; _st_t = _t; }
-#define MIB_STAMP_FLUSH(cond) if (cond) { for (int _i = 0; _i < 6; _i++) atomicAdd(&g_stamps[_i], _st_acc[_i]); \
-  atomicAdd(&g_stamps[6], __builtin_amdgcn_s_memtime() - _st_t0); atomicAdd(&g_stamps[7], __builtin_amdgcn_s_memrealtime() - _st_r0); \
-  atomicAdd(&g_stamps[8], 1ull); }
+#define MIB_STAMP_FLUSH(cond, slot) if (cond) { for (int _i = 0; _i < 8; _i++) atomicAdd(&g_stamps[8 * (slot) + _i], _st_acc[_i]); \
+  atomicAdd(&g_stamps[16], __builtin_amdgcn_s_memtime() - _st_t0); atomicAdd(&g_stamps[17], __builtin_amdgcn_s_memrealtime() - _st_r0); \
+  atomicAdd(&g_stamps[18], 1ull); }
 #else
 #define MIB_STAMP_INIT
 #define MIB_STAMP(i)
-#define MIB_STAMP_FLUSH(cond)
+#define MIB_STAMP_FLUSH(cond, slot)
 #endif
 
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }

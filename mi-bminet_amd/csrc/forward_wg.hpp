@@ -684,12 +684,13 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     // being hoisted out of the loop (they would be live across it and spill)
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    MIB_STAMP(5)
+    MIB_STAMP(7)
     __builtin_amdgcn_s_setprio(PRIO_L1);
     layer1<K>(xt, xn, smem + K::OFF_Y1, R, wave, lane);
     __builtin_amdgcn_s_setprio(0);
-    MIB_LOOP_BARRIER();  // A
     MIB_STAMP(0)
+    MIB_LOOP_BARRIER();  // A
+    MIB_STAMP(1)
     const LaneTab T = ((const LaneTab*)(smem + K::OFF_LT))[ln];
 #ifndef MIB_DIAG_NOL2
     layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, T, wave, ln);
@@ -702,27 +703,29 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
-    MIB_STAMP(1)
+    MIB_STAMP(2)
 #ifndef MIB_DIAG_NOL3
     layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, T, wave);
 #endif
+    MIB_STAMP(3)
     MIB_LOOP_BARRIER();  // B
-    MIB_STAMP(2)
+    MIB_STAMP(4)
     if (wave == NWAVES - 1) {
       __builtin_amdgcn_s_setprio(PRIO_L45);
 #ifdef MIB_DIAG_NOL45
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = *(const unsigned*)(smem + K::OFF_Y3 + 4 * (b & 15));
 #else
       layer4<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, ln);
-      MIB_STAMP(3)
+      MIB_STAMP(5)
       const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, ln);
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = z;
 #endif
       __builtin_amdgcn_s_setprio(0);
+      MIB_STAMP(6)
     }
-    MIB_STAMP(4)
   }
-  MIB_STAMP_FLUSH(tid == 64 * (NWAVES - 1))
+  MIB_STAMP_FLUSH(tid == 0, 0)
+  MIB_STAMP_FLUSH(tid == 64 * (NWAVES - 1), 1)
 }
 
 // Single-trial, single-layer kernel for the reference's per-layer entry points (debug/parity):

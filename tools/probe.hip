@@ -22,24 +22,27 @@ int main(int argc, char** argv) {
   hipMemcpy(x, hx.data(), hx.size(), hipMemcpyHostToDevice);
   rc = net_model_compute_batch(x, y, B, 0);
   if (rc) { printf("run rc %d %s\n", rc, net_error_string(rc)); return 1; }
-  unsigned long long zero[16] = {0};
+  unsigned long long zero[24] = {0};
   hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero));
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   hipEventRecord(e0, 0);
   for (int i = 0; i < iters; i++) net_model_compute_batch_async(x, y, B, 0, nullptr);
   hipEventRecord(e1, 0); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
-  unsigned long long st[16];
+  unsigned long long st[24];
   hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
   int32_t info[3]; net_launch_info(B, 0, info);
-  const char* names[] = {"layer1", "layer2", "layer3", "layer4", "layer5+store", "loop top", "-", "-"};
+  const char* names[] = {"layer1 work", "barrier A wait", "layer2 work", "layer3 work", "barrier B wait",
+                         "layer4 (last wave)", "layer5 (last wave)", "loop top"};
   double trials = (double)B * iters;
   printf("B=%zu iters=%d  %.3f ms/launch  grid %d  lds %d\n", B, iters, ms / iters, info[0], info[2]);
-  double tot = 0;
-  for (int i = 0; i < 6; i++) tot += st[i];
-  printf("  shader clock from s_memtime/s_memrealtime: %.3f GHz\n", 0.1 * (double)st[6] / (double)st[7]);
-  for (int i = 0; i < 6; i++)
-    printf("  %-18s %8.0f cycles/trial/flusher  (%4.1f%%)\n", names[i], st[i] / trials, 100.0 * st[i] / tot);
-  printf("  total %8.0f cycles per trial per flusher (s_memtime ticks), flushers %llu\n", tot / trials, st[8]);
+  printf("  shader clock from s_memtime/s_memrealtime: %.3f GHz\n", 0.1 * (double)st[16] / (double)st[17]);
+  printf("  %-20s %12s %12s   (cycles per trial, summed over the trial's wave)\n", "phase", "wave 0", "last wave");
+  double t0 = 0, t1 = 0;
+  for (int i = 0; i < 8; i++) {
+    printf("  %-20s %12.0f %12.0f\n", names[i], st[i] / trials, st[8 + i] / trials);
+    t0 += st[i]; t1 += st[8 + i];
+  }
+  printf("  %-20s %12.0f %12.0f\n", "total", t0 / trials, t1 / trials);
   return 0;
 }
