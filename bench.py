@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--config", default="b22", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--per-launch-events", action="store_true",
+                    help="bracket every launch with its own HIP events (diagnostic; adds idle gaps)")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="target CPU-baseline wall time")
     ap.add_argument("--pcie", action="store_true",
                     help="also time the host-buffer path (pinned H2D + forward + D2H); reported as "
@@ -148,18 +150,29 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    # HIP events on the launch stream bracket the K back-to-back launches (an event pair around
+    # every launch leaves the GPU idle between launches: about +10 % per step on config B);
+    # --per-launch-events keeps that mode for diagnostics
+    nev = a.steps if a.per_launch_events else 1
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        ev[i][0].record(stream)
-        step()
-        ev[i][1].record(stream)
+    if a.per_launch_events:
+        for i in range(a.steps):
+            ev[i][0].record(stream)
+            step()
+            ev[i][1].record(stream)
+    else:
+        ev[0][0].record(stream)
+        for i in range(a.steps):
+            step()
+        ev[0][1].record(stream)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = [s.elapsed_time(e) for s, e in ev]
+    kernel_ms = ([s.elapsed_time(e) for s, e in ev] if a.per_launch_events
+                 else [ev[0][0].elapsed_time(ev[0][1]) / a.steps])
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
