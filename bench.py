@@ -123,11 +123,15 @@ def main():
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
     dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", init_method="env://")
+    # RCCL ("nccl") between the ranks; MIB_BENCH_BACKEND=gloo lets several ranks share one GPU
+    # (rehearsal of the multi-rank path on a one-GPU box)
+    backend = os.environ.get("MIB_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group(backend, init_method="env://")
 
     ps = ParamSet.synthetic(seed=a.seed, C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"])
     lib.params_load(ps)
@@ -174,7 +178,7 @@ def main():
     kernel_ms = ([s.elapsed_time(e) for s, e in ev] if a.per_launch_events
                  else [ev[0][0].elapsed_time(ev[0][1]) / a.steps])
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
