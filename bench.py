@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--config", default="b22", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--settle", type=float, default=0.25,
+                    help="seconds of untimed launches before the warmup steps (GPU clock ramp)")
     ap.add_argument("--per-launch-events", action="store_true",
                     help="bracket every launch with its own HIP events (diagnostic; adds idle gaps)")
     ap.add_argument("--cpu-seconds", type=float, default=25.0, help="target CPU-baseline wall time")
@@ -148,6 +150,14 @@ def main():
     def step():
         lib.model_compute_batch(x.data_ptr(), y.data_ptr(), B, local, sp)
 
+    # settle (untimed, before the W warmup steps): from idle the GPU clock needs some tens of ms
+    # of load to reach its steady state; without this the first ~50 ms run about 7 % slower
+    # (measured: W = 5 -> 0.467 ms/step, W = 50 or 200 -> 0.436-0.439 ms/step on config B)
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < a.settle:
+        for _ in range(20):
+            step()
+        torch.cuda.synchronize(dev)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -203,6 +213,7 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
+            "settle_s": a.settle,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
