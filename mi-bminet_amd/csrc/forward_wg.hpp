@@ -310,7 +310,11 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
 #pragma unroll
   for (int t = 0; t < K::P; t++) {  // both N-tiles' MFMAs before either requant
     const L1Tile& T = R.tile(t);
+#ifdef MIB_DIAG_NOL1MFMA
+    accs[t] = a + T.wf;
+#else
     accs[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, T.wf, (v4i){T.ci, T.ci, T.ci, T.ci}, 0, 0, 0);
+#endif
   }
 #pragma unroll
   for (int t = 0; t < K::P; t++) {
@@ -479,7 +483,14 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
       for (int i = 0; i < 16; i++) acc[i] = K::RB ? 0 : R.thr2[fi];  // plain branch: C-init
 #pragma unroll
       for (int s = 0; s < 3; s++)
+#ifdef MIB_DIAG_NOL2MFMA
+      {
+        const v4i bb = *(const v4i*)(pb + l2_boff<K>(s, 0));
+        acc[s] += bb[0]; acc[4 + s] += bb[1]; acc[8 + s] += bb[2]; acc[12 + s] += bb[3];
+      }
+#else
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, 0)), acc, 0, 0, 0);
+#endif
       // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
 #ifdef MIB_DIAG_NOPOOL
       const unsigned w = acc[0] ^ acc[5] ^ acc[10] ^ acc[15];
@@ -646,7 +657,8 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
 // Diagnostics only (tools/probe.hip and tools/ab.py builds; all give wrong results, for timing
 // insight): MIB_DIAG_NOBAR drops the in-loop barriers, MIB_DIAG_SAME_TRIAL makes every trial read
 // trial 0 (L2-resident), MIB_DIAG_NOL1RQ / NOPOOL / NOTAIL / NOL2 / NOL3 / NOL45 skip the
-// layer-1 requant, the layer-2 pooling, the layer-2 tail tile, layer 2, layer 3, layers 4-5.
+// layer-1 requant, the layer-2 pooling, the layer-2 tail tile, layer 2, layer 3, layers 4-5;
+// MIB_DIAG_NOL1MFMA / NOL2MFMA replace the layer-1 / layer-2 full-tile MFMAs by a vector add.
 #ifdef MIB_DIAG_NOBAR
 #define MIB_LOOP_BARRIER() ((void)0)
 #else
