@@ -143,6 +143,7 @@ struct LaneTab {
   int l3w;  // layer-3 store: y3_off(16 col + 4 g), or -1 (rows past T8)
   int pad;
 };
+static_assert(sizeof(SmallParams) % 16 == 0, "SmallParams is copied to LDS in 16-byte pieces");
 
 // byte offset of y3t row u (see Cfg::Y3S)
 template <class K>
@@ -761,6 +762,11 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
   __syncthreads();
   if (stage == 1) {  // [T][C] packed (XTRIAL bytes) -> [F1][T_ALIGN]
     prefetch_l1<K>(in, R, wave, lane);
+    // All fragment loads land before layer 1 starts.  With them still in flight, this single-
+    // workgroup path gave a wrong layer-1 row in ~2 % of calls on gfx950 (tools/stress.py; the
+    // batched kernel, whose fragments are loaded a whole trial ahead, showed none in 39 M trials).
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
     layer1<K>(in, in, y1, R, wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T_AL; i += NTHREADS) {
