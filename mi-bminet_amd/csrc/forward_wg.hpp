@@ -198,39 +198,10 @@ struct Regs {
   float r2[FPW];
   long a3[FPW];            // layer-3 band fragments of the wave's filters
   v4i pf[K::PF];           // layer-1 fragments prefetched one trial ahead
+  int xoff;                // lane_xoff(lane)
 };
 
 // ---- layer-1 input ---------------------------------------------------------------------------
-// A fragment of block `blk` (16 time groups): lane (j, g) holds bytes
-// [ (16 blk + j) * GS + 16 g, +16 ) of the trial.  Unconditional, branch-free loads (a branch
-// around a load makes the compiler drain vmcnt at the join); blocks past the end are clamped to
-// the last block, windows running past the trial are clamped to its last 16 bytes and shifted
-// back into place by fix_a().
-template <class K>
-__device__ __forceinline__ int a_offset(int blk, int lane) {
-  return (blk * 16 + (lane & 15)) * K::GS + 16 * (lane >> 4);
-}
-
-template <class K>
-__device__ __forceinline__ v4i load_a(const int8_t* __restrict__ xt, int blk, int lane) {
-  const int b = blk < K::NB1 ? blk : K::NB1 - 1;
-  const int off = min(a_offset<K>(b, lane), K::XTRIAL - 16);
-  return __builtin_nontemporal_load((const v4i*)(xt + off));
-}
-
-template <class K>
-__device__ __forceinline__ v4i fix_a(v4i v, int blk, int lane) {
-  if (blk != K::NB1 - 1) return v;  // wave-uniform; only the last block can run past the trial
-  const int k = (a_offset<K>(blk, lane) - (K::XTRIAL - 16)) >> 2;  // dwords to shift down
-  if (k <= 0) return v;
-  v4i r;
-  r.x = k == 1 ? v.y : k == 2 ? v.z : k == 3 ? v.w : 0;
-  r.y = k == 1 ? v.z : k == 2 ? v.w : 0;
-  r.z = k == 1 ? v.w : 0;
-  r.w = 0;
-  return r;
-}
-
 // Layer-1 blocks of a wave: a contiguous range (see l1_split).  Slots past the wave's count
 // repeat its last block (the loads stay unconditional, the compute is skipped).
 template <class K>
@@ -252,10 +223,47 @@ __device__ __forceinline__ int l1_blk(int wave, int i) {
   return b < 0 ? 0 : (b > K::NB1 - 1 ? K::NB1 - 1 : b);
 }
 
+// A fragment of block `blk` (16 time groups): lane (j, g) holds bytes
+// [ (16 blk + j) * GS + 16 g, +16 ) of the trial.  The loads are raw buffer loads through a
+// descriptor per (trial, wave): base = the wave's first block, num_records = the bytes left in the
+// batch from there.  The hardware range check is per dword (tools/buf_probe.hip), so windows
+// running past the batch's last trial read zeros instead of faulting, and there is no per-trial
+// address arithmetic: the lane offset is loop-invariant and slot i adds 16 * GS * i (the
+// instruction's immediate offset while it fits in 12 bits).  Windows past a trial's end read the
+// next trial's bytes; those meet zero weights (the pad K-slots) or belong to samples >= T, which
+// l1_block masks to zero.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+
+// trials_left: trials of the batch from xt on (<= 0: an empty view)
 template <class K>
-__device__ __forceinline__ void prefetch_l1(const int8_t* __restrict__ xt, Regs<K>& R, int wave, int lane) {
+__device__ __forceinline__ Rsrc trial_rsrc(const int8_t* xt, int trials_left, int wave) {
+  const int wb = l1_start<K>(wave) * 16 * K::GS;  // byte offset of the wave's first block
+  constexpr int TMAX = 0x7fffffff / K::XTRIAL;     // more trials than this: num_records saturates
+  const int nrec = trials_left <= 0 ? 0 : trials_left >= TMAX ? 0x7fffffff : max(trials_left * K::XTRIAL - wb, 0);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(xt + wb), (short)0, nrec, 0x00020000);
+}
+
+template <class K>
+__device__ __forceinline__ int lane_xoff(int lane) {
+  return (lane & 15) * K::GS + 16 * (lane >> 4);
+}
+
+// slot i of the wave (block l1_start + i); slots past the wave's count read data nobody uses
+template <class K>
+__device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * 16 * K::GS, 0, 2 /* nt */);
+  return (v4i)v;
+}
+
+template <class K>
+__device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R) {
+  // laundered: otherwise xoff + 16 GS i is hoisted out of the trial loop into a register per slot
+  // instead of riding in the loads' immediate offsets
+  int xo = R.xoff;
+  asm volatile("" : "+v"(xo));
 #pragma unroll
-  for (int i = 0; i < K::PF; i++) R.pf[i] = load_a<K>(xt, l1_blk<K>(wave, i), lane);
+  for (int i = 0; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, i);
 }
 
 template <class K>
@@ -264,6 +272,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
 #pragma unroll
   for (int t = 0; t < K::P; t++) {
     L1Tile& T = R.tile(t);
+    R.xoff = lane_xoff<K>(lane);
     T.wf = prm->l1_wfrag[t][lane];
     T.ci = prm->l1_cinit[t][lane & 15];
     T.rr = prm->l1_r[t][lane & 15];
@@ -348,29 +357,27 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
 }
 
 // Layer 1: x[T][C] (HBM, via R.pf) -> y1 rows (LDS, position 32 + t).  Prefetches the next
-// trial's fragments (xnext) into R.pf once the current ones are consumed.
+// trial's fragments (rnext) into R.pf once the current ones are consumed.
 template <class K>
-__device__ __forceinline__ void layer1(const int8_t* __restrict__ xt, const int8_t* __restrict__ xnext,
-                                       int8_t* smem_y1, Regs<K>& R, int wave, int lane) {
+__device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, Regs<K>& R, int wave, int lane) {
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
   v4i xa[NX > 0 ? NX : 1];
 #pragma unroll
-  for (int i = 0; i < NX; i++) xa[i] = load_a<K>(xt, l1_blk<K>(wave, K::PF + i), lane);
+  for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
 #pragma unroll
   for (int i = 0; i < K::NBW; i++) {
     if (i < n) {  // wave-uniform
       const int blk = l1_blk<K>(wave, i);
       v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
-      if (blk == K::NB1 - 1) {  // the trial's last block: windows past the end, samples >= T
-        a = fix_a<K>(a, blk, lane);
+      if (blk == K::NB1 - 1) {  // the trial's last block: samples >= T are masked
         l1_block<K, true>(a, blk, smem_y1, R, lane);
       } else {
         l1_block<K, false>(a, blk, smem_y1, R, lane);
       }
     }
   }
-  prefetch_l1<K>(xnext, R, wave, lane);
+  prefetch_l1<K>(rnext, R);
 }
 
 // ---- layer 2 ---------------------------------------------------------------------------------
@@ -667,8 +674,10 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
 #endif
 #ifdef MIB_DIAG_SAME_TRIAL
 #define MIB_TRIAL_OFF(b) ((size_t)0 * (size_t)(b))
+#define MIB_TRIALS_LEFT(b) ((int)(b) < B ? 1 : 0)
 #else
 #define MIB_TRIAL_OFF(b) ((size_t)(b) * K::XTRIAL)
+#define MIB_TRIALS_LEFT(b) (B - (int)(b))
 #endif
 
 // Fused forward over a batch (persistent, grid-strided over trials).
@@ -681,7 +690,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   Regs<K> R;
   setup<K>(prm, smem, R, tid, wave, lane);
   const SmallParams* sp = (const SmallParams*)(smem + K::OFF_SP);
-  if ((int)blockIdx.x < B) prefetch_l1<K>(x + (size_t)blockIdx.x * K::XTRIAL, R, wave, lane);
+  if ((int)blockIdx.x < B)
+    prefetch_l1<K>(trial_rsrc<K>(x + MIB_TRIAL_OFF(blockIdx.x), MIB_TRIALS_LEFT(blockIdx.x), wave), R);
   __syncthreads();
   MIB_STAMP_INIT
   // Per trial two barriers: A after layer 1 (layer 2 of a filter reads all waves' layer-1
@@ -691,15 +701,15 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   // nor y4, and its layer 3 comes after the next A, which the last wave reaches only when done.
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const int bn = b + gridDim.x;
-    const int8_t* xt = x + MIB_TRIAL_OFF(b);
-    const int8_t* xn = bn < B ? x + MIB_TRIAL_OFF(bn) : xt;  // last: harmless re-read
+    const Rsrc rc = trial_rsrc<K>(x + MIB_TRIAL_OFF(b), MIB_TRIALS_LEFT(b), wave);
+    const Rsrc rn = trial_rsrc<K>(x + MIB_TRIAL_OFF(bn), MIB_TRIALS_LEFT(bn), wave);  // bn >= B: empty
     // laundered lane id: per-lane addresses of layers 2-5 are recomputed every trial instead of
     // being hoisted out of the loop (they would be live across it and spill)
     int ln = lane;
     asm volatile("" : "+v"(ln));
     MIB_STAMP(7)
     __builtin_amdgcn_s_setprio(PRIO_L1);
-    layer1<K>(xt, xn, smem + K::OFF_Y1, R, wave, lane);
+    layer1<K>(rc, rn, smem + K::OFF_Y1, R, wave, lane);
     __builtin_amdgcn_s_setprio(0);
     MIB_STAMP(0)
     MIB_LOOP_BARRIER();  // A
@@ -761,13 +771,14 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
   int8_t* y4 = smem + K::OFF_Y4;
   __syncthreads();
   if (stage == 1) {  // [T][C] packed (XTRIAL bytes) -> [F1][T_ALIGN]
-    prefetch_l1<K>(in, R, wave, lane);
+    const Rsrc rin = trial_rsrc<K>(in, 1, wave);
+    prefetch_l1<K>(rin, R);
     // All fragment loads land before layer 1 starts.  With them still in flight, this single-
     // workgroup path gave a wrong layer-1 row in ~2 % of calls on gfx950 (tools/stress.py; the
     // batched kernel, whose fragments are loaded a whole trial ahead, showed none in 39 M trials).
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    layer1<K>(in, in, y1, R, wave, lane);
+    layer1<K>(rin, rin, y1, R, wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T_AL; i += NTHREADS) {
       const int f = i / T_AL, t = i - f * T_AL;
