@@ -46,7 +46,13 @@ static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wa
 // Wave priorities (s_setprio): the last wave's layers 4-5 are the longest dependency chain of the
 // layer-1 interval, so that wave issues first while on them; layer 1 (HBM fragments, next-trial
 // prefetch) goes ahead of the other workgroup's layers 2-3.  Same-box A/B: -4 %.
-constexpr int PRIO_L1 = 1, PRIO_L45 = 3;
+#ifndef MIB_PRIO_L1
+#define MIB_PRIO_L1 1
+#endif
+#ifndef MIB_PRIO_L45
+#define MIB_PRIO_L45 3
+#endif
+constexpr int PRIO_L1 = MIB_PRIO_L1, PRIO_L45 = MIB_PRIO_L45;
 
 // Layer-1 work split.  The last wave also runs layers 4 and 5 (in the same barrier interval as
 // the next trial's layer 1), so it takes fewer layer-1 blocks: waves 0 .. NWAVES-2 get cm blocks
@@ -245,6 +251,12 @@ __device__ __forceinline__ Rsrc trial_rsrc(const int8_t* xt, int trials_left, in
 
 template <class K>
 __device__ __forceinline__ int lane_xoff(int lane) {
+#ifndef MIB_NO_ZERO_PAD_LANES
+  // A lane whose 16-byte chunk lies wholly past the group's P * C bytes (C = 22: bytes 48..63)
+  // only meets zero weights: it reads past num_records instead (offset >= 2^31 > any
+  // num_records), so the hardware returns zeros without fetching and the MFMA multiplies zeros.
+  if (16 * (lane >> 4) >= K::GS) return (int)0x80000000u;
+#endif
   return (lane & 15) * K::GS + 16 * (lane >> 4);
 }
 
