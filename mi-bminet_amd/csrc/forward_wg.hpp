@@ -231,21 +231,23 @@ __device__ __forceinline__ int l1_blk(int wave, int i) {
 
 // A fragment of block `blk` (16 time groups): lane (j, g) holds bytes
 // [ (16 blk + j) * GS + 16 g, +16 ) of the trial.  The loads are raw buffer loads through a
-// descriptor per (trial, wave): base = the wave's first block, num_records = the bytes left in the
-// batch from there.  The hardware range check is per dword (tools/buf_probe.hip), so windows
-// running past the batch's last trial read zeros instead of faulting, and there is no per-trial
+// descriptor per (trial, wave): base = the wave's first block, num_records = the wave's own bytes
+// (see trial_rsrc).  The hardware range check is per dword (tools/buf_probe.hip), so windows
+// running past them read zeros instead of faulting or fetching, and there is no per-trial
 // address arithmetic: the lane offset is loop-invariant and slot i adds 16 * GS * i (the
-// instruction's immediate offset while it fits in 12 bits).  Windows past a trial's end read the
-// next trial's bytes; those meet zero weights (the pad K-slots) or belong to samples >= T, which
-// l1_block masks to zero.
+// instruction's immediate offset while it fits in 12 bits).  Samples >= T of the last block are
+// masked to zero by l1_block.
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 
-// trials_left: trials of the batch from xt on (<= 0: an empty view)
+// The view ends where the wave's own bytes end: its last group's P * C bytes, or the trial's end.
+// Window bytes past a group's own data meet zero weights, so reading them as zeros changes
+// nothing, and no wave fetches the next trial's bytes (slots past its block count, windows past
+// the trial's end) from memory.  trials_left <= 0: an empty view.
 template <class K>
 __device__ __forceinline__ Rsrc trial_rsrc(const int8_t* xt, int trials_left, int wave) {
   const int wb = l1_start<K>(wave) * 16 * K::GS;  // byte offset of the wave's first block
-  constexpr int TMAX = 0x7fffffff / K::XTRIAL;     // more trials than this: num_records saturates
-  const int nrec = trials_left <= 0 ? 0 : trials_left >= TMAX ? 0x7fffffff : max(trials_left * K::XTRIAL - wb, 0);
+  const int own = min(l1_count<K>(wave) * 16 * K::GS, K::XTRIAL - wb);
+  const int nrec = trials_left <= 0 ? 0 : max(own, 0);
   return __builtin_amdgcn_make_buffer_rsrc((void*)(xt + wb), (short)0, nrec, 0x00020000);
 }
 

@@ -51,23 +51,40 @@ def main():
                 open(f"{prof}/{tag}_bench_{cfg}.json", "w").write(lines[-1])
     fetch = pmc_values(one(f"{src}/pmc_fetch/**/*counter_collection.csv"), "FETCH_SIZE")
     write = pmc_values(one(f"{src}/pmc_write/**/*counter_collection.csv"), "WRITE_SIZE")
+    rqf = glob.glob(f"{src}/pmc_rdreq/**/*counter_collection.csv", recursive=True)
+    rcols = ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
+    rvals = {c: pmc_values(rqf[0], c) for c in rcols} if rqf else {c: [] for c in rcols}
     with open(f"{prof}/{tag}_pmc.csv", "w") as f:
-        f.write("dispatch,FETCH_SIZE_kB,WRITE_SIZE_kB\n")
-        for i in range(max(len(fetch), len(write))):
-            fv = fetch[i] if i < len(fetch) else ""
-            wv = write[i] if i < len(write) else ""
-            f.write(f"{i},{fv},{wv}\n")
+        f.write("dispatch,FETCH_SIZE_kB,WRITE_SIZE_kB," + ",".join(rcols) + "\n")
+        for i in range(max(len(fetch), len(write), *(len(v) for v in rvals.values()))):
+            row = [fetch[i] if i < len(fetch) else "", write[i] if i < len(write) else ""]
+            row += [rvals[c][i] if i < len(rvals[c]) else "" for c in rcols]
+            f.write(f"{i}," + ",".join(str(x) for x in row) + "\n")
     # skip the first (warm-up) dispatch
-    fk = sorted(fetch[1:] or fetch)[len(fetch[1:] or fetch) // 2]
-    wk = sorted(write[1:] or write)[len(write[1:] or write) // 2]
-    read_bytes = 2 * fk * 1024
+    med = lambda v: sorted(v[1:] or v)[len(v[1:] or v) // 2]  # noqa: E731
+    fk = med(fetch)
+    wk = med(write)
     write_bytes = wk * 1024
     tj = {"config": "b22", "batch": 65536, "kernel": "k_forward<Cfg<22,1125>>",
-          "fetch_size_kB_raw": fk, "write_size_kB": wk,
-          "read_bytes_corrected": read_bytes, "write_bytes": write_bytes,
-          "hbm_bytes_per_launch": read_bytes + write_bytes,
-          "alg_bytes_per_launch": (22 * 1125 + 4) * 65536,
-          "source": f"profiles/{tag}_pmc.csv (median over dispatches after the first; FETCH_SIZE x2 per gfx950 correction)"}
+          "fetch_size_kB_raw": fk, "write_size_kB": wk, "write_bytes": write_bytes,
+          "alg_bytes_per_launch": (22 * 1125 + 4) * 65536}
+    rq = glob.glob(f"{src}/pmc_rdreq/**/*counter_collection.csv", recursive=True)
+    if rq:
+        # memory-side read requests by size: bytes = 32 n32 + 64 n64 + 128 n128 (the requests of
+        # other sizes, if any, are reported as the remainder and not counted)
+        n = {c: med(pmc_values(rq[0], c)) for c in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum",
+                                                     "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")}
+        read_bytes = 32 * n["TCC_EA0_RDREQ_32B_sum"] + 64 * n["TCC_EA0_RDREQ_64B_sum"] + 128 * n["TCC_EA0_RDREQ_128B_sum"]
+        tj.update({"rdreq": n, "rdreq_other": n["TCC_EA0_RDREQ_sum"] - n["TCC_EA0_RDREQ_32B_sum"]
+                   - n["TCC_EA0_RDREQ_64B_sum"] - n["TCC_EA0_RDREQ_128B_sum"],
+                   "read_bytes": read_bytes, "read_bytes_fetch_size_x2": 2 * fk * 1024,
+                   "source": f"profiles/{tag}_pmc.csv (medians over dispatches after the first); reads from "
+                             "TCC_EA0_RDREQ_{32B,64B,128B}_sum (bytes by request size), writes WRITE_SIZE"})
+    else:
+        read_bytes = 2 * fk * 1024
+        tj.update({"read_bytes": read_bytes,
+                   "source": f"profiles/{tag}_pmc.csv (median over dispatches after the first; FETCH_SIZE x2 per gfx950 correction)"})
+    tj["hbm_bytes_per_launch"] = read_bytes + write_bytes
     json.dump(tj, open(f"{prof}/pmc_traffic.json", "w"), indent=1)
     # agreement check: rocprofv3 kernel-trace durations of the timed dispatches vs the HIP-event
     # average bench.py measured in the same (profiled) process
@@ -77,7 +94,7 @@ def main():
     prof_line = [l for l in open(f"{src}/trace.log") if l.startswith("{")][-1]
     pb = json.loads(prof_line)
     steps, warm = pb["steps"], pb["warmup"]
-    timed = durs[warm:warm + steps]
+    timed = durs[-steps:]  # the timed launches are the process's last `steps` dispatches (after settle + warmup)
     summary = {
         "kernel": tj["kernel"],
         "rocprof_dispatches": len(durs),
