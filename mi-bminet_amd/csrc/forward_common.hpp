@@ -82,7 +82,9 @@ struct DevParams {
   int l2_off[F2];
   float l2_r[F2];
   long l3_afrag[F2][64];    // layer-3 A operand (16 shifts x 32-byte band) per filter and lane
-  v4i l2t_afrag[F2][2][64]; // layer-2 tail A operand (16 shifts x 128-slot band, MFMA 16x16x64)
+  // layer-2 tail A operand per filter pair (wave) and K-step: MFMA 16x16x64, 16 shifts x 192
+  // K-slots = the two filters' 96-slot bands side by side (K block diagonal, see forward_wg.hpp)
+  v4i l2t_afrag[F2 / 2][3][64];
   SmallParams sp;
 };
 

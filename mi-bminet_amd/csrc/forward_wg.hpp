@@ -119,8 +119,8 @@ struct Cfg {
   static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S + 4 * (Y3ROWS >> 4));
   static constexpr int OFF_SP = OFF_Y4 + align16(64 * N5L);
   static constexpr int OFF_LT = align16(OFF_SP + (int)sizeof(SmallParams));   // per-lane offsets
-  static constexpr int OFF_L2T = OFF_LT + 64 * 32;                            // tail band fragments
-  static constexpr int LDS = OFF_L2T + (TB > 0 ? F2 * 2 * 64 * 16 : 0);
+  static constexpr int OFF_L2T = OFF_LT + 64 * 48;                            // tail band fragments
+  static constexpr int LDS = OFF_L2T + (TB > 0 ? NWAVES * 3 * 64 * 16 : 0);
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
   static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
   static_assert(T64 >= 1, "T >= 64");
@@ -142,13 +142,15 @@ __device__ __forceinline__ int y1_index(int f, int t) {
 struct LaneTab {
   int l2b;  // full tile, B slice (filter 0, tile 0, K-step 0): (32 / P) c + l2_boff(0, h)
   int l2y;  // full tile, y2 store (filter 0, tile 0): 8 + 4 c + 2 h
-  int tb;   // tail B window: fi_c * Y1ROW + window offset of (col, g)
+  int tb[3];  // tail B chunk of K-step s (offset within the wave's filter pair; a zero chunk when
+             // the K-step's slots of this lane belong to the other filter)
   int ty;   // tail y2 store: fi_c * Y2ROW + 8 + u, or -1 (lane stores nothing)
   int tp;   // tail: filter slot fi_c of this lane's column (0 or 1)
   int l3b;  // layer-3 B slice: 16 col + 8 g
   int l3w;  // layer-3 store: y3_off(16 col + 4 g), or -1 (rows past T8)
-  int pad;
+  int pad[3];
 };
+static_assert(sizeof(LaneTab) == 48, "LaneTab is read as three 16-byte pieces");
 static_assert(sizeof(SmallParams) % 16 == 0, "SmallParams is copied to LDS in 16-byte pieces");
 
 // byte offset of y3t row u (see Cfg::Y3S)
@@ -167,6 +169,22 @@ __device__ __forceinline__ int l2_boff(int s, int h) {
   else return 32 * s + 16 * h;
 }
 
+// Layer-2 tail window chunks.  Column (fi, bq) of the tail covers outputs 1024 MT + 16 bq + m
+// (m < 16), which read row positions p0 + q, p0 = 1024 MT + 16 bq, q = m + 1 + tap <= 79.  The
+// window is cut into 16-byte chunks mq = 0..5 of the row: P == 2: plane mq & 1, plane bytes
+// p0 / 2 + 16 (mq >> 1) .. +15 (positions q = 32 (mq >> 1) + 2 jj + (mq & 1)); P == 1: bytes
+// p0 + 16 mq .. +15 (q = 16 mq + jj; chunk 5 is never needed and reads zeros).  The host builds
+// the band fragments (l2t_afrag) with the same slot -> position map.
+template <class K>
+__device__ __host__ constexpr int tail_q(int mq, int jj) {
+  return K::P == 2 ? 32 * (mq >> 1) + 2 * jj + (mq & 1) : 16 * mq + jj;
+}
+template <class K>
+__device__ __forceinline__ int tail_chunk_off(int fi, int bq, int mq) {
+  if constexpr (K::P == 2) return fi * K::Y1ROW + (mq & 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (mq >> 1);
+  else return mq < 5 ? fi * K::Y1ROW + 1024 * K::MT + 16 * bq + 16 * mq : 0;
+}
+
 template <class K>
 __device__ __forceinline__ LaneTab build_lane_tab(int lane) {
   LaneTab T;
@@ -180,8 +198,13 @@ __device__ __forceinline__ LaneTab build_lane_tab(int lane) {
     const int fi_c = K::TC > 0 ? col / cmax(K::TC, 1) : 0, bq = col - fi_c * K::TC;
     const bool cvalid = fi_c < FPW;
     const int fs = cvalid ? fi_c : 0;
-    T.tb = fs * K::Y1ROW + ((K::P == 2) ? (g >> 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (g & 1)
-                                         : 1024 * K::MT + 16 * bq + 16 * g);
+#pragma unroll
+    for (int st = 0; st < 3; st++) {
+      const int kap = 4 * st + g, kf = kap / 6, mq = kap - 6 * kf;  // chunk kap = filter kf's chunk mq
+      int off = 0;  // zero chunk: plane bytes 0..15 of the pair's first row (positions < 32 are pads)
+      if (cvalid && kf == fi_c) off = tail_chunk_off<K>(fi_c, bq, mq);
+      T.tb[st] = off;
+    }
     const int u = 128 * K::MT + 2 * bq + (g >> 1);
     T.ty = (cvalid && !(g & 1) && u < K::T8) ? fs * K::Y2ROW + 8 + u : -1;
     T.tp = fs;
@@ -189,7 +212,7 @@ __device__ __forceinline__ LaneTab build_lane_tab(int lane) {
     const int u3 = 16 * col + 4 * g;
     T.l3w = u3 < K::T8 ? y3_off<K>(u3) : -1;
   }
-  T.pad = 0;
+  T.pad[0] = T.pad[1] = T.pad[2] = 0;
   return T;
 }
 
@@ -316,7 +339,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   if constexpr (K::TB > 0) {
     const v4i* t = &prm->l2t_afrag[0][0][0];
     v4i* d = (v4i*)(smem + K::OFF_L2T);
-    for (int i = tid; i < F2 * 2 * 64; i += NTHREADS) d[i] = t[i];
+    for (int i = tid; i < NWAVES * 3 * 64; i += NTHREADS) d[i] = t[i];
   }
   // everything else zero: layer-1 pads (positions [0,32) and past the last block), layer-2 pads
   // ([0,8) and [8+T8, Y2ROW)) and the zero row are never rewritten
@@ -422,47 +445,33 @@ __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, fl
   return sat8x2((int)q[0], (int)q[1]);
 }
 
-// Layer-2 tail: outputs 1024 MT + 16 bq + m (m < 16) of the wave's filters.  Column col =
-// TC fi + bq belongs to filter fi.  Per filter two MFMA i32_16x16x64_i8 (K-steps s = 0, 1: window
-// positions 0..127; taps reach position 79), A = the filter's 16-shift band (LDS).  B = every
-// lane's own column, read once and multiplied by both filters' bands; each lane keeps the
-// accumulator of its own filter.  P == 2: lane (col, g), step s reads parity plane g >> 1, plane
-// bytes 32 s + 16 (g & 1) .. +15 of the column's window.  Slots past position 79 meet zero
-// weights, so the window may run into the next plane / row.  D lane (col, g) holds shifts
-// 4g .. 4g+3: half of pool window g >> 1; lanes g and g ^ 1 are rows 2k, 2k+1 of the wave and
-// meet by v_permlane16_swap.
+// Layer-2 tail: outputs 1024 MT + 16 bq + m (m < 16) of the wave's two filters, one column of 16
+// outputs per lane column col = TC fi + bq (filter fi).  One chain of three MFMA i32_16x16x64_i8
+// with a block-diagonal K: K-slots 0..95 carry filter 0's window chunks and band, slots 96..191
+// filter 1's (chunk kap = 4 s + g of K-step s and lane group g, see build_lane_tab), and a lane
+// whose column belongs to the other filter reads a zero chunk there.  Every column so gets its own
+// filter's sums and no MFMA work is thrown away.  D lane (col, g) holds shifts 4g .. 4g+3: half of
+// pool window g >> 1; lanes g and g ^ 1 meet by v_permlane16_swap (layer2_tail_out).
 template <class K>
 __device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const SmallParams* sp, const LaneTab& T,
                                                 int wave, int lane) {
-  const v4i* tA = (const v4i*)(smem_y1 - K::OFF_Y1 + K::OFF_L2T);
-  constexpr int SOFF = K::P == 2 ? 32 : 64;  // B byte offset of K-step 1
-  const int8_t* pb = smem_y1 + wave * FPW * K::Y1ROW + T.tb;
-  v4i bv[2];
+  const v4i* tA = (const v4i*)(smem_y1 - K::OFF_Y1 + K::OFF_L2T) + wave * 3 * 64 + lane;
+  const int8_t* pb = smem_y1 + wave * FPW * K::Y1ROW;
+  v4i bv[3], a[3];
 #pragma unroll
-  for (int s = 0; s < 2; s++) {
-    const long* q = (const long*)(pb + SOFF * s);  // 8-byte aligned
+  for (int st = 0; st < 3; st++) {
+    const long* q = (const long*)(pb + T.tb[st]);  // 8-byte aligned
     const long lo = q[0], hi = q[1];
-    bv[s][0] = (int)lo; bv[s][1] = (int)(lo >> 32); bv[s][2] = (int)hi; bv[s][3] = (int)(hi >> 32);
+    bv[st][0] = (int)lo; bv[st][1] = (int)(lo >> 32); bv[st][2] = (int)hi; bv[st][3] = (int)(hi >> 32);
+    a[st] = tA[st * 64];
   }
-  v4i acc[FPW], a[FPW][2];
+  v4i acc = {0, 0, 0, 0};
 #pragma unroll
-  for (int fi = 0; fi < FPW; fi++) {
-    const int f = wave * FPW + fi;
-    const int ci = K::RB ? 0 : sp->l2n_ci[f];
-    acc[fi] = (v4i){ci, ci, ci, ci};
-#pragma unroll
-    for (int s = 0; s < 2; s++) {
-      a[fi][s] = tA[(2 * f + s) * 64 + lane];
-      acc[fi] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[fi][s], bv[s], acc[fi], 0, 0, 0);
-    }
-  }
-  // Operands stay live until the results are ready.  A version mixing 16x16x64 and 16x16x32
-  // steps in these chains gave wrong tail sums on gfx950 for some register allocations, while
-  // the same sequences in isolation (tools/mfma_hazard*.hip) were correct; see DESIGN.md.
-  asm volatile("" : "+v"(acc[0]), "+v"(acc[1]) : "v"(a[0][0]), "v"(a[0][1]), "v"(a[1][0]), "v"(a[1][1]), "v"(bv[0]),
-               "v"(bv[1]));
-  static_assert(FPW == 2, "two accumulators");
-  return T.tp == 0 ? acc[0] : acc[1];
+  for (int st = 0; st < 3; st++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[st], bv[st], acc, 0, 0, 0);
+  // Operands stay live until the result is ready (see DESIGN.md on the tail chains).
+  asm volatile("" : "+v"(acc) : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(bv[0]), "v"(bv[1]), "v"(bv[2]));
+  if constexpr (!K::RB) acc += sp->l2n_ci[wave * FPW + T.tp];  // plain branch: magic-offset C-init
+  return acc;
 }
 
 template <class K>

@@ -256,20 +256,6 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         }
         std::memcpy(&dp.l2_afrag[f][s][lane], bytes, 16);
       }
-    // tail band for MFMA 16x16x64: lane (m, g), K-step s holds slots 64 s + 16 g + jj; slot ->
-    // window position q as the device reads B (P == 2: plane g >> 1, plane byte 32 s + 16 (g & 1)
-    // + jj); row m = output shift, tap q - m - 1
-    for (int s = 0; s < 2; s++)
-      for (int lane = 0; lane < 64; lane++) {
-        const int m = lane & 15, g = lane >> 4;
-        int8_t bytes[16];
-        for (int jj = 0; jj < 16; jj++) {
-          const int q = P == 2 ? 2 * (32 * s + 16 * (g & 1) + jj) + (g >> 1) : 64 * s + 16 * g + jj;
-          const int idx = q - m - 1;
-          bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
-        }
-        std::memcpy(&dp.l2t_afrag[f][s][lane], bytes, 16);
-      }
     dp.l2_thr[f] = -(hp.l2_offset[f] >> 3);
     dp.l2_off[f] = hp.l2_offset[f];
     if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f])) return NET_ERR_RANGE;
@@ -278,6 +264,23 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     dp.sp.l2_r[f] = dp.l2_r[f];
 
   }
+  // layer-2 tail bands (forward_wg.hpp, layer2_tail_mfma): filter pair w = filters 2w, 2w+1;
+  // lane (m, g) of K-step s holds K-slots 64 s + 16 g + jj = chunk kap = 4 s + g, byte jj, which
+  // is chunk mq = kap - 6 kf of filter kf = kap / 6; its window position q (tail_q) meets tap
+  // q - m - 1 of the output shift m.
+  for (int w = 0; w < F2 / 2; w++)
+    for (int s = 0; s < 3; s++)
+      for (int lane = 0; lane < 64; lane++) {
+        const int m = lane & 15, g = lane >> 4, kap = 4 * s + g, kf = kap / 6, mq = kap - 6 * kf;
+        const int f = 2 * w + kf;
+        int8_t bytes[16];
+        for (int jj = 0; jj < 16; jj++) {
+          const int q = P == 2 ? 32 * (mq >> 1) + 2 * jj + (mq & 1) : 16 * mq + jj;
+          const int idx = q - m - 1;
+          bytes[jj] = (int8_t)((idx >= 0 && idx < 64 && (P == 2 || mq < 5)) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
+        }
+        std::memcpy(&dp.l2t_afrag[w][s][lane], bytes, 16);
+      }
   SmallParams& sp = dp.sp;
   // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed.
   // A operand of MFMA i32_16x16x32_i8: row r (output shift within a block of 16), K-slot k (byte
