@@ -119,7 +119,8 @@ struct Cfg {
   static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S + 4 * (Y3ROWS >> 4));
   static constexpr int OFF_SP = OFF_Y4 + align16(64 * N5L);
   static constexpr int OFF_LT = align16(OFF_SP + (int)sizeof(SmallParams));   // per-lane offsets
-  static constexpr int OFF_L2T = OFF_LT + 64 * 48;                            // tail band fragments
+  static constexpr int OFF_L45 = OFF_LT + 64 * 48;                            // layer-4/5 lane offsets
+  static constexpr int OFF_L2T = OFF_L45 + 64 * 32;                           // tail band fragments
   static constexpr int LDS = OFF_L2T + (TB > 0 ? NWAVES * 3 * 64 * 16 : 0);
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
   static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
@@ -151,12 +152,45 @@ struct LaneTab {
   int pad[3];
 };
 static_assert(sizeof(LaneTab) == 48, "LaneTab is read as three 16-byte pieces");
+
 static_assert(sizeof(SmallParams) % 16 == 0, "SmallParams is copied to LDS in 16-byte pieces");
 
 // byte offset of y3t row u (see Cfg::Y3S)
 template <class K>
-__device__ __forceinline__ int y3_off(int u) {
+__host__ __device__ constexpr int y3_off(int u) {
   return u * K::Y3S + 4 * (u >> 4);
+}
+
+// Per-lane offsets of layers 4 and 5 (the last wave), built once per workgroup like LaneTab: the
+// wave re-reads them after barrier B instead of recomputing them from the lane id every trial.
+struct L45Tab {
+  int l4a;  // y3_off(32 h + n(i)): layer-4 A row of part 0 (part t adds y3_off(64 t))
+  int l4w;  // k T64A + 4 (i >> 4) + 2 h: layer-4 store of part 0 (part t adds 8 t)
+  int l4k;  // 4 k: byte offset of output channel k in the per-channel parameter arrays
+  int l4m;  // bit t set when part t's store lies inside the row (v < T64A)
+  int l5y;  // 4 c: layer-5 input dword of lane (n, c) (dword j adds 16 dwords)
+  int l5w;  // 4 (n ND5_MAX + c): its weight
+  int l5n;  // 4 n: class n's bias
+  int pad;
+};
+
+template <class K>
+__device__ __forceinline__ L45Tab build_l45_tab(int lane) {
+  L45Tab L;
+  const int i = lane & 31, h = lane >> 5, k = i & 15;
+  const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
+  const int vl = 4 * (i >> 4) + 2 * h;
+  L.l4a = y3_off<K>(32 * h + n);
+  L.l4w = k * K::T64A + vl;
+  L.l4k = 4 * k;
+  L.l4m = 0;
+  for (int t = 0; t < K::NT4; t++) L.l4m |= (8 * t + vl < K::T64A) << t;
+  const int n5 = lane >> 4, c = lane & 15;
+  L.l5y = 4 * c;
+  L.l5w = 4 * (n5 * ND5_MAX + c);
+  L.l5n = 4 * n5;
+  L.pad = 0;
+  return L;
 }
 
 // layer-2 B operand: byte offset (within a filter's rows, column block 0) of the 16-byte slice of
@@ -336,6 +370,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   v4i* dst = (v4i*)(smem + K::OFF_SP);
   for (int i = tid; i < (int)(sizeof(SmallParams) / 16); i += NTHREADS) dst[i] = src[i];
   if (tid < 64) ((LaneTab*)(smem + K::OFF_LT))[tid] = build_lane_tab<K>(tid);
+  if (tid < 64) ((L45Tab*)(smem + K::OFF_L45))[tid] = build_l45_tab<K>(tid);
   if constexpr (K::TB > 0) {
     const v4i* t = &prm->l2t_afrag[0][0][0];
     v4i* d = (v4i*)(smem + K::OFF_L2T);
@@ -590,17 +625,19 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
 // c >= 16: channel c-16 on slots 16..31), so column c of D = channel c & 15 of time block c >> 4.
 // Rows n(i) permuted so lane (c, h) register r = time 16h + r of that block: two pool-8 windows.
 template <class K>
-__device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* sp, int k) {
+__device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* sp, int kb) {
+  // kb = 4 k (byte offset of channel k)
+#define MIB_K4(arr, T) (*(const T*)((const char*)(arr) + kb))
   if constexpr (K::RB) {
-    const int thr = sp->l4_thr[k], off = sp->l4_off[k];
-    const float r4 = sp->l4_r[k];
+    const int thr = MIB_K4(sp->l4_thr, int), off = MIB_K4(sp->l4_off, int);
+    const float r4 = MIB_K4(sp->l4_r, float);
     const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
     return sat8x2((int)q[0], (int)q[1]);
   } else {
     // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
     // sum of 8, >> 3, clip.  Elements are clamped to [0, 1024]: any element >= 1024 already
     // saturates the result, and the reciprocal is verified exact up to there.
-    const float rn = sp->l4n_r[k], cn = sp->l4n_c[k];
+    const float rn = MIB_K4(sp->l4n_r, float), cn = MIB_K4(sp->l4n_c, float);
     int sm[2];
 #pragma unroll
     for (int hw = 0; hw < 2; hw++) {
@@ -623,15 +660,14 @@ __device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* s
 // L4PIPE: software-pipelined by one part (the MFMA of part t+1 is issued before the pooling of
 // part t, two accumulators live); otherwise one part at a time.
 template <class K>
-__device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, const SmallParams* sp, int lane) {
-  const int i = lane & 31, h = lane >> 5, k = i & 15;
-  const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
+__device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, const SmallParams* sp, const L45Tab& L,
+                                       int lane) {
   const v4i bw = sp->l4_bfrag[lane];
-  const int ci = K::RB ? 0 : sp->l4n_ci[k];  // plain branch: C-init
+  const int ci = K::RB ? 0 : *(const int*)((const char*)sp->l4n_ci + L.l4k);  // plain branch: C-init
   if constexpr (K::L4PIPE) {
     v4i a[K::NT4];
 #pragma unroll
-    for (int t = 0; t < K::NT4; t++) a[t] = *(const v4i*)(smem_y3 + y3_off<K>(64 * t + 32 * h + n));  // unaligned (4 B)
+    for (int t = 0; t < K::NT4; t++) a[t] = *(const v4i*)(smem_y3 + L.l4a + y3_off<K>(64 * t));  // unaligned (4 B)
     v16i acc[2];
 #pragma unroll
     for (int j = 0; j < 16; j++) acc[0][j] = ci;
@@ -643,41 +679,38 @@ __device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, c
         for (int j = 0; j < 16; j++) acc[(t + 1) & 1][j] = ci;
         acc[(t + 1) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[t + 1 < K::NT4 ? t + 1 : 0], bw, acc[(t + 1) & 1], 0, 0, 0);
       }
-      const unsigned w = l4_out<K>(acc[t & 1], sp, k);
-      const int v0 = 8 * t + 4 * (i >> 4) + 2 * h;  // even
-      if (v0 < K::T64A) *(unsigned short*)(smem_y4 + k * K::T64A + v0) = (unsigned short)w;
+      const unsigned w = l4_out<K>(acc[t & 1], sp, L.l4k);
+      if ((L.l4m >> t) & 1) *(unsigned short*)(smem_y4 + L.l4w + 8 * t) = (unsigned short)w;
     }
   } else {
 #pragma unroll
     for (int t = 0; t < K::NT4; t++) {
-      const v4i a = *(const v4i*)(smem_y3 + y3_off<K>(64 * t + 32 * h + n));  // unaligned (4 B)
+      const v4i a = *(const v4i*)(smem_y3 + L.l4a + y3_off<K>(64 * t));  // unaligned (4 B)
       v16i acc;
 #pragma unroll
       for (int j = 0; j < 16; j++) acc[j] = ci;
       acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bw, acc, 0, 0, 0);
-      const unsigned w = l4_out<K>(acc, sp, k);
-      const int v0 = 8 * t + 4 * (i >> 4) + 2 * h;  // even
-      if (v0 < K::T64A) *(unsigned short*)(smem_y4 + k * K::T64A + v0) = (unsigned short)w;
+      const unsigned w = l4_out<K>(acc, sp, L.l4k);
+      if ((L.l4m >> t) & 1) *(unsigned short*)(smem_y4 + L.l4w + 8 * t) = (unsigned short)w;
     }
   }
 }
 
 // ---- layer 5 ---------------------------------------------------------------------------------
 template <class K>
-__device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallParams* sp, int lane) {
-  const int n = lane >> 4, c = lane & 15;
+__device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallParams* sp, const L45Tab& L) {
   int part = 0;
 #pragma unroll
-  for (int j = 0; j < K::N5L; j++) {
-    const int i = c + 16 * j;  // pad columns and dwords past ND5 meet zero weights
-    part = __builtin_amdgcn_sdot4(*(const int*)(smem_y4 + 4 * i), sp->l5_w[n][i], part, false);
+  for (int j = 0; j < K::N5L; j++) {  // dword c + 16 j of class n (pad columns and dwords past ND5 meet zero weights)
+    part = __builtin_amdgcn_sdot4(*(const int*)(smem_y4 + L.l5y + 64 * j),
+                                  *(const int*)((const char*)sp->l5_w + L.l5w + 64 * j), part, false);
   }
   // inclusive prefix sum within each 16-lane DPP row: lane 15 of the row holds the total
   part += __builtin_amdgcn_update_dpp(0, part, 0x111, 0xF, 0xF, true);  // row_shr:1
   part += __builtin_amdgcn_update_dpp(0, part, 0x112, 0xF, 0xF, true);  // row_shr:2
   part += __builtin_amdgcn_update_dpp(0, part, 0x114, 0xF, 0xF, true);  // row_shr:4
   part += __builtin_amdgcn_update_dpp(0, part, 0x118, 0xF, 0xF, true);  // row_shr:8
-  const int z = rq(part + sp->l5_b[n], sp->l5_r);
+  const int z = rq(part + *(const int*)((const char*)sp->l5_b + L.l5n), sp->l5_r);
   const unsigned z0 = (unsigned)__builtin_amdgcn_readlane(z, 15) & 255u;
   const unsigned z1 = (unsigned)__builtin_amdgcn_readlane(z, 31) & 255u;
   const unsigned z2 = (unsigned)__builtin_amdgcn_readlane(z, 47) & 255u;
@@ -761,9 +794,10 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
 #ifdef MIB_DIAG_NOL45
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = *(const unsigned*)(smem + K::OFF_Y3 + 4 * (b & 15));
 #else
-      layer4<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, ln);
+      const L45Tab L = ((const L45Tab*)(smem + K::OFF_L45))[ln];
+      layer4<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, L, ln);
       MIB_STAMP(5)
-      const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, ln);
+      const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, L);
       if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = z;
 #endif
       __builtin_amdgcn_s_setprio(0);
@@ -835,7 +869,7 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
     for (int i = tid; i < K::Y3ROWS * F2; i += NTHREADS) y3[y3_off<K>(i / F2) + (i % F2)] = i < K::T8 * F2 ? in[i] : 0;
     __syncthreads();
     if (wave == 0)
-      layer4<K>(y3, y4, sp, lane);
+      layer4<K>(y3, y4, sp, ((const L45Tab*)(smem + K::OFF_L45))[lane], lane);
     __syncthreads();
     for (int i = tid; i < F2 * T64_AL; i += NTHREADS) {
       const int k = i / T64_AL, v = i - k * T64_AL;
@@ -848,7 +882,7 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
     }
     __syncthreads();
     if (wave == 0) {
-      const unsigned z = layer5<K>(y4, sp, lane);
+      const unsigned z = layer5<K>(y4, sp, ((const L45Tab*)(smem + K::OFF_L45))[lane]);
       if (lane == 0) *(unsigned*)out = z;
     }
   } else if (stage == 6) {  // flip [F2][T8_ALIGN] -> [T8][F2] (net_layer3_flip_inplace)
