@@ -86,6 +86,13 @@ def main():
                    "source": f"profiles/{tag}_pmc.csv (median over dispatches after the first; FETCH_SIZE x2 per gfx950 correction)"})
     tj["hbm_bytes_per_launch"] = read_bytes + write_bytes
     json.dump(tj, open(f"{prof}/pmc_traffic.json", "w"), indent=1)
+    # the config-B bench line of this round carries this round's traffic (bench.py read the
+    # previous pmc_traffic.json when it ran, before these counter passes)
+    bp = f"{prof}/{tag}_bench_b22.json"
+    if os.path.exists(bp):
+        bl = json.loads(open(bp).read())
+        bl["roofline"]["traffic"] = tj["hbm_bytes_per_launch"]
+        open(bp, "w").write(json.dumps(bl) + "\n")
     # agreement check: rocprofv3 kernel-trace durations of the timed dispatches vs the HIP-event
     # average bench.py measured in the same (profiled) process
     trace = one(f"{src}/trace/**/*kernel_trace.csv")
