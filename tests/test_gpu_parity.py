@@ -133,3 +133,22 @@ def test_reload_params_between_calls(gpu):
     for seed in (1, 2, 1):
         ps = ParamSet.synthetic(seed=seed)
         np.testing.assert_array_equal(run_batch(ps, x), oracle.COracle(ps).batch(x))
+
+
+def test_batch_past_2gib(gpu):
+    """B = 100,000 trials (2.48 GB of input, trial offsets past 2^31 bytes): sampled parity,
+    including the batch's last trials (whose layer-1 windows run past the end of the input)."""
+    torch = _torch()
+    B = 100_000
+    ps = ParamSet.synthetic(seed=99, stress=True)
+    lib.params_load(ps)
+    stride = lib.trial_stride()
+    assert B * stride > 2**31
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randint(-128, 128, (B, stride), dtype=torch.int8, device="cuda", generator=g)
+    x[:, 22 * 1125:] = 0
+    y = lib.forward_torch(x)
+    torch.cuda.synchronize()
+    idx = np.concatenate([np.random.default_rng(1).choice(B - 64, 192, replace=False), np.arange(B - 64, B)])
+    want = oracle.COracle(ps).batch(x[torch.from_numpy(idx).cuda()].cpu().numpy(), nthreads=8)
+    np.testing.assert_array_equal(y.cpu().numpy()[idx], want)
