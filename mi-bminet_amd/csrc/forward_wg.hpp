@@ -52,6 +52,9 @@ static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wa
 #ifndef MIB_PRIO_L45
 #define MIB_PRIO_L45 3
 #endif
+#ifndef MIB_PRIO_L23_LAST
+#define MIB_PRIO_L23_LAST 0
+#endif
 constexpr int PRIO_L1 = MIB_PRIO_L1, PRIO_L45 = MIB_PRIO_L45;
 
 // Layer-1 work split.  The last wave also runs layers 4 and 5 (in the same barrier interval as
@@ -763,6 +766,12 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     // being hoisted out of the loop (they would be live across it and spill)
     int ln = lane;
     asm volatile("" : "+v"(ln));
+#ifdef MIB_L1WAIT_STAMP
+    // diagnostic: wait for this trial's prefetched fragments here, so that stamp slot 7 holds the
+    // part of the HBM latency the previous trial did not cover
+    MIB_STAMP(6)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
     MIB_STAMP(7)
     __builtin_amdgcn_s_setprio(PRIO_L1);
     layer1<K>(rc, rn, smem + K::OFF_Y1, R, wave, lane);
@@ -771,6 +780,11 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     MIB_LOOP_BARRIER();  // A
     MIB_STAMP(1)
     const LaneTab T = ((const LaneTab*)(smem + K::OFF_LT))[ln];
+#if MIB_PRIO_L23_LAST
+    // the last wave is the youngest of its SIMD: at equal priority it loses the arbitration in
+    // layers 2-3 and reaches barrier B last, on the path to its layers 4-5
+    if (wave == NWAVES - 1) __builtin_amdgcn_s_setprio(MIB_PRIO_L23_LAST);
+#endif
 #ifndef MIB_DIAG_NOL2
     layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, T, wave, ln);
 #endif
