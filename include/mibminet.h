@@ -75,7 +75,9 @@ int net_last_error(void);
 /* Load a parameter blob (format: mi-bminet_amd/mibminet/params.py, ParamSet.to_blob): the
  * net.h arrays net_l1_factor ... net_l5_weight with their dimensions, int8 or packed int4
  * weights, and the build variant (flag bit 0: -DREORDER_BN, the canonical build; clear: the plain
- * BN branches of layer2.c:139-210 / layer4.c:91-133).  Validates, precomputes the gfx950 operand fragments and exact requantisation
+ * BN branches of layer2.c:139-210 / layer4.c:91-133.  Flag bit 1: clip every requantised output to
+ * [-127, 127], the golden model's clip_balanced=True, functional.py:89-91; clear: [-128, 127] as
+ * the C's __CLIP_R).  Other flag bits are rejected (NET_ERR_BLOB).  Validates, precomputes the gfx950 operand fragments and exact requantisation
  * reciprocals, and uploads lazily to each device on first use.  Replaces any previous set. */
 int net_params_load(const void* blob, size_t len);
 

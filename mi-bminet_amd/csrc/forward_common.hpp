@@ -88,21 +88,34 @@ struct DevParams {
   SmallParams sp;
 };
 
+// LO: lower clip bound, -128 (the C's __CLIP_R(x, 127), clip_balanced=False) or -127
+// (golden_model.py clip_balanced=True, functional.py:89-91)
+template <int LO = -128>
 __device__ __forceinline__ int rq(int v, float r) {
   const int t = (int)((float)v * r);
-  return min(max(t, -128), 127);
+  return min(max(t, LO), 127);
 }
 
 // int32 -> saturated int8 pairs (gfx950 v_ashr_pk_i8_i32, shift 0): a to byte 0, b to byte 1.
 // The op_sel form writes bytes 2/3 and keeps bytes 0/1 (checked on hardware by
 // tools/isa_probe.hip).
+template <int LO = -128>
 __device__ __forceinline__ unsigned sat8x2(int a, int b) {
+  if constexpr (LO != -128) {  // the pack saturates at -128 only
+    a = max(a, LO);
+    b = max(b, LO);
+  }
   unsigned r;
   asm("v_ashr_pk_i8_i32 %0, %1, %2, 0" : "=v"(r) : "v"(a), "v"(b));
   return r;
 }
+template <int LO = -128>
 __device__ __forceinline__ unsigned sat8x4(int a, int b, int c, int d) {
-  unsigned r = sat8x2(a, b);
+  if constexpr (LO != -128) {
+    c = max(c, LO);
+    d = max(d, LO);
+  }
+  unsigned r = sat8x2<LO>(a, b);
   asm("v_ashr_pk_i8_i32 %0, %1, %2, 0 op_sel:[0,0,0,1]" : "+v"(r) : "v"(c), "v"(d));
   return r;
 }

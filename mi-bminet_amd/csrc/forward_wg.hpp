@@ -81,10 +81,12 @@ constexpr L1Split l1_split(int nb1) {
   return best;
 }
 
-template <int C_, int T_, bool RB_ = true>
+template <int C_, int T_, bool RB_ = true, bool CB_ = false>
 struct Cfg {
   static constexpr int C = C_, T = T_;
   static constexpr bool RB = RB_;                       // -DREORDER_BN variant (canonical)
+  static constexpr bool CB = CB_;                       // golden-model clip_balanced: clip to [-127, 127]
+  static constexpr int LO = CB ? -127 : -128;           // lower clip bound of every requant
   static constexpr int P = (C <= 32) ? 2 : 1;          // samples per 64-byte L1 window
   static constexpr int GS = P * C;                      // bytes per time group
   static constexpr int NB1 = (T + 16 * P - 1) / (16 * P);  // L1 blocks of 16 groups
@@ -427,7 +429,7 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
       for (int r = 0; r < 4; r++) y[r] = (K::P * (16 * blk + 4 * g + r) + p < K::T) ? y[r] : 0;
     }
     const int t0 = K::P * (16 * blk + 4 * g) + p;  // first of the lane's 4 samples (stride P)
-    *(unsigned*)(smem_y1 + y1_index<K>(f, t0)) = sat8x4(y[0], y[1], y[2], y[3]);
+    *(unsigned*)(smem_y1 + y1_index<K>(f, t0)) = sat8x4<K::LO>(y[0], y[1], y[2], y[3]);
   }
 }
 
@@ -478,9 +480,10 @@ __device__ __forceinline__ unsigned l2n_out(const v16i& acc, float r, float c) {
 }
 
 // Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].
+template <int LO>
 __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, float r) {
   const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r, r};
-  return sat8x2((int)q[0], (int)q[1]);
+  return sat8x2<LO>((int)q[0], (int)q[1]);
 }
 
 // Layer-2 tail: outputs 1024 MT + 16 bq + m (m < 16) of the wave's two filters, one column of 16
@@ -530,7 +533,7 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
   const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)part, (unsigned)part, false, false);
   const int tot = (int)sw[0] + (int)sw[1];  // whole window (rows 2k and 2k+1 hold the same)
   int y;
-  if constexpr (K::RB) y = rq(tot + sp->l2_off[fcol], sp->l2_r[fcol]);
+  if constexpr (K::RB) y = rq<K::LO>(tot + sp->l2_off[fcol], sp->l2_r[fcol]);
   else y = tot >> 3;
   if (T.ty >= 0) smem_y2[wave * FPW * K::Y2ROW + T.ty] = (int8_t)y;
 }
@@ -564,7 +567,7 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 #ifdef MIB_DIAG_NOPOOL
       const unsigned w = acc[0] ^ acc[5] ^ acc[10] ^ acc[15];
 #else
-      const unsigned w = K::RB ? l2_out(acc, R.thr2[fi], R.off2[fi], R.r2[fi])
+      const unsigned w = K::RB ? l2_out<K::LO>(acc, R.thr2[fi], R.off2[fi], R.r2[fi])
                                : l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
 #endif
       int8_t* dst = smem_y2 + f * K::Y2ROW + 128 * mt + T.l2y;
@@ -606,7 +609,7 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
     acc = __builtin_amdgcn_mfma_i32_16x16x32_i8(R.a3[fi], bv, acc, 0, 0, 0);
     const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(acc[0]), __int_as_float(acc[1])}, (f2){r3, r3}, (f2){c3, c3});
     const f2 q23 = __builtin_elementwise_fma((f2){__int_as_float(acc[2]), __int_as_float(acc[3])}, (f2){r3, r3}, (f2){c3, c3});
-    w[fi] = sat8x4((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
+    w[fi] = sat8x4<K::LO>((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
   }
   // interleave the two filters: pair i = bytes (f0[i], f1[i])
   const unsigned p01 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u);  // f0[0] f1[0] f0[1] f1[1]
@@ -635,7 +638,7 @@ __device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* s
     const int thr = MIB_K4(sp->l4_thr, int), off = MIB_K4(sp->l4_off, int);
     const float r4 = MIB_K4(sp->l4_r, float);
     const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
-    return sat8x2((int)q[0], (int)q[1]);
+    return sat8x2<K::LO>((int)q[0], (int)q[1]);
   } else {
     // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
     // sum of 8, >> 3, clip.  Elements are clamped to [0, 1024]: any element >= 1024 already
@@ -713,7 +716,7 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
   part += __builtin_amdgcn_update_dpp(0, part, 0x112, 0xF, 0xF, true);  // row_shr:2
   part += __builtin_amdgcn_update_dpp(0, part, 0x114, 0xF, 0xF, true);  // row_shr:4
   part += __builtin_amdgcn_update_dpp(0, part, 0x118, 0xF, 0xF, true);  // row_shr:8
-  const int z = rq(part + *(const int*)((const char*)sp->l5_b + L.l5n), sp->l5_r);
+  const int z = rq<K::LO>(part + *(const int*)((const char*)sp->l5_b + L.l5n), sp->l5_r);
   const unsigned z0 = (unsigned)__builtin_amdgcn_readlane(z, 15) & 255u;
   const unsigned z1 = (unsigned)__builtin_amdgcn_readlane(z, 31) & 255u;
   const unsigned z2 = (unsigned)__builtin_amdgcn_readlane(z, 47) & 255u;

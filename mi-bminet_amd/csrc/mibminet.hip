@@ -30,6 +30,7 @@ namespace {
 constexpr int MAX_DEVICES = 64;
 constexpr int HEADER_SIZE = 64;
 constexpr uint32_t FLAG_REORDER_BN = 1;
+constexpr uint32_t FLAG_CLIP_BALANCED = 2;  // golden-model clip_balanced=True (functional.py:89-91)
 
 struct Dims {
   int C = 0, T = 0, F1 = 0, F2 = 0, D = 0, N = 0, wbits = 8;
@@ -48,6 +49,7 @@ struct HostParams {
   std::vector<int8_t> l1_weight_align, l2_weight_reverse, l3_weight, l4_weight, l5_bias, l5_weight;
   int32_t l3_factor = 0, l5_factor = 0;
   bool reorder_bn = true;  // blob flag: -DREORDER_BN variant (canonical) or the plain BN branches
+  bool clip_balanced = false;  // blob flag: clip to [-127, 127] (golden model's default; the C clips to -128)
 };
 
 // ---- exact requantisation ------------------------------------------------------------------
@@ -165,7 +167,9 @@ int parse_blob(const void* blob, size_t len, HostParams& hp) {
   d.N = (int)h[6]; d.wbits = (int)h[7];
   const uint32_t l2t = h[8], l3t = h[9], flags = h[10];
   if (version != 1 || l2t != 64 || l3t != 16) return NET_ERR_BLOB;
+  if (flags & ~(FLAG_REORDER_BN | FLAG_CLIP_BALANCED)) return NET_ERR_BLOB;
   hp.reorder_bn = (flags & FLAG_REORDER_BN) != 0;
+  hp.clip_balanced = (flags & FLAG_CLIP_BALANCED) != 0;
   if (d.wbits != 8 && d.wbits != 4) return NET_ERR_BLOB;
   if (d.C <= 0 || d.T < 64 || d.F1 <= 0 || d.N <= 0 || d.F2 != d.F1 * d.D) return NET_ERR_BLOB;
   Reader r{b, len, (size_t)HEADER_SIZE};
@@ -329,18 +333,39 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
 }
 
 // ---- compiled configurations --------------------------------------------------------------
-using CfgB = wg::Cfg<22, 1125>;  // BCI-IV-2a: 22 channels x 1125 samples (configs A, B, D, E)
-using CfgC = wg::Cfg<64, 1000>;  // high-density variant: 64 channels x 1000 samples (config C)
-using CfgBn = wg::Cfg<22, 1125, false>;  // the same networks built without -DREORDER_BN
-using CfgCn = wg::Cfg<64, 1000, false>;
-
-enum class Variant { None, B22x1125, C64x1000, B22x1125n, C64x1000n };
+// Two shapes, 22 x 1125 (BCI-IV-2a: configs A, B, D, E) and 64 x 1000 (config C), each compiled
+// with and without -DREORDER_BN and with both clip modes: wg::Cfg<C, T, RB, CB>.
+struct Variant {
+  int shape = -1;  // 0: 22 x 1125, 1: 64 x 1000, -1: unsupported
+  bool rb = true;  // -DREORDER_BN branches (canonical)
+  bool cb = false; // golden-model clip_balanced (clip to [-127, 127])
+  bool ok() const { return shape >= 0; }
+};
 
 Variant variant_of(const HostParams& hp) {
   const Dims& d = hp.d;
-  if (d.C == 22 && d.T == 1125) return hp.reorder_bn ? Variant::B22x1125 : Variant::B22x1125n;
-  if (d.C == 64 && d.T == 1000) return hp.reorder_bn ? Variant::C64x1000 : Variant::C64x1000n;
-  return Variant::None;
+  Variant v;
+  if (d.C == 22 && d.T == 1125) v.shape = 0;
+  else if (d.C == 64 && d.T == 1000) v.shape = 1;
+  v.rb = hp.reorder_bn;
+  v.cb = hp.clip_balanced;
+  return v;
+}
+
+template <int C, int T, class F>
+int with_variant(const Variant& v, F&& f) {
+  if (v.rb) return v.cb ? f(wg::Cfg<C, T, true, true>{}) : f(wg::Cfg<C, T, true, false>{});
+  return v.cb ? f(wg::Cfg<C, T, false, true>{}) : f(wg::Cfg<C, T, false, false>{});
+}
+
+// Calls f(K{}) with the kernel configuration K of the variant.
+template <class F>
+int dispatch(const Variant& v, F&& f) {
+  switch (v.shape) {
+    case 0: return with_variant<22, 1125>(v, f);
+    case 1: return with_variant<64, 1000>(v, f);
+    default: return NET_ERR_UNSUPPORTED;
+  }
 }
 
 size_t trial_stride(const Dims& d) { return ((size_t)d.C * d.T + 15) / 16 * 16; }
@@ -438,34 +463,16 @@ int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_
   return hip_err(hipGetLastError());
 }
 
-int launch_forward(Variant v, DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y,
+int launch_forward(const Variant& v, DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y,
                    size_t B, hipStream_t st, int32_t* info = nullptr) {
-  switch (v) {
-    case Variant::B22x1125: return launch_forward_t<CfgB>(ds, p, x, y, B, st, info);
-    case Variant::C64x1000: return launch_forward_t<CfgC>(ds, p, x, y, B, st, info);
-    case Variant::B22x1125n: return launch_forward_t<CfgBn>(ds, p, x, y, B, st, info);
-    case Variant::C64x1000n: return launch_forward_t<CfgCn>(ds, p, x, y, B, st, info);
-    default: return NET_ERR_UNSUPPORTED;
-  }
+  return dispatch(v, [&](auto k) { return launch_forward_t<decltype(k)>(ds, p, x, y, B, st, info); });
 }
 
-int launch_layer(Variant v, const DevParams* p, const int8_t* in, int8_t* out, int stage) {
-  switch (v) {
-    case Variant::B22x1125:
-      hipLaunchKernelGGL(wg::k_layer<CfgB>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
-      break;
-    case Variant::C64x1000:
-      hipLaunchKernelGGL(wg::k_layer<CfgC>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
-      break;
-    case Variant::B22x1125n:
-      hipLaunchKernelGGL(wg::k_layer<CfgBn>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
-      break;
-    case Variant::C64x1000n:
-      hipLaunchKernelGGL(wg::k_layer<CfgCn>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
-      break;
-    default: return NET_ERR_UNSUPPORTED;
-  }
-  return hip_err(hipGetLastError());
+int launch_layer(const Variant& v, const DevParams* p, const int8_t* in, int8_t* out, int stage) {
+  return dispatch(v, [&](auto k) {
+    hipLaunchKernelGGL(wg::k_layer<decltype(k)>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
+    return hip_err(hipGetLastError());
+  });
 }
 
 // Runs one reference-layout single-trial stage on the single-trial device.
@@ -476,7 +483,7 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
   if (!s.host) return NET_ERR_NO_PARAMS;
   const Dims& d = s.host->d;
   const Variant v = variant_of(*s.host);
-  if (v == Variant::None) return NET_ERR_UNSUPPORTED;
+  if (!v.ok()) return NET_ERR_UNSUPPORTED;
   const int dev = g_single_device;
   DeviceState& ds = g_devs[dev];
   std::lock_guard<std::mutex> lk(ds.mu);
@@ -554,7 +561,7 @@ int net_params_load(const void* blob, size_t len) {
   auto hp = std::make_shared<HostParams>();
   int rc = parse_blob(blob, len, *hp);
   if (rc) return rc;
-  if (variant_of(*hp) == Variant::None) return NET_ERR_UNSUPPORTED;
+  if (!variant_of(*hp).ok()) return NET_ERR_UNSUPPORTED;
   auto dp = std::make_shared<DevParams>();
   rc = build_devparams(*hp, *dp);
   if (rc) return rc;
@@ -605,7 +612,7 @@ int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int devi
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
   const Variant v = variant_of(*s.host);
-  if (v == Variant::None) return NET_ERR_UNSUPPORTED;
+  if (!v.ok()) return NET_ERR_UNSUPPORTED;
   DeviceState& ds = g_devs[device];
   std::lock_guard<std::mutex> lk(ds.mu);
   DeviceGuard guard(device);

@@ -28,7 +28,7 @@ class _Params(ctypes.Structure):
         ("l3_factor", ctypes.c_int32), ("l3_weight", ctypes.c_void_p),
         ("l4_factor", ctypes.c_void_p), ("l4_offset", ctypes.c_void_p), ("l4_weight", ctypes.c_void_p),
         ("l5_factor", ctypes.c_int32), ("l5_bias", ctypes.c_void_p), ("l5_weight", ctypes.c_void_p),
-        ("reorder_bn", ctypes.c_int32),
+        ("reorder_bn", ctypes.c_int32), ("clip_lo", ctypes.c_int32),
     ]
 
 
@@ -70,7 +70,8 @@ class COracle:
                          ptr(ps.l2_factor), ptr(ps.l2_offset), ptr(ps.l2_weight_reverse),
                          ps.l3_factor, ptr(ps.l3_weight),
                          ptr(ps.l4_factor), ptr(ps.l4_offset), ptr(ps.l4_weight),
-                         ps.l5_factor, ptr(ps.l5_bias), ptr(ps.l5_weight), int(getattr(ps, "reorder_bn", True)))
+                         ps.l5_factor, ptr(ps.l5_bias), ptr(ps.l5_weight), int(getattr(ps, "reorder_bn", True)),
+                         -127 if getattr(ps, "clip_balanced", False) else -128)
         self.pref = ctypes.byref(self.p)
         self.L = lib()
 

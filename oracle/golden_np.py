@@ -1,7 +1,7 @@
 """TEST INFRASTRUCTURE ONLY — NumPy restatement of the reference golden model.
 
-Restates ``edge-eegnet_wolf/python_utils/golden_model.py`` (``GoldenModel(clip_balanced=False,
-reorder_bn=True)``, Layer1..Layer5 at :153-379) and the functional ops it uses
+Restates ``edge-eegnet_wolf/python_utils/golden_model.py`` (``GoldenModel(clip_balanced=...,
+reorder_bn=...)`` with both flags taken from the ParamSet, Layer1..Layer5 at :153-379) and the functional ops it uses
 (``python_utils/functional.py``), vectorised over a batch of trials.  It is independent of the C
 restatement (oracle.c): the two are cross-checked on every fixture, and both are pinned by
 SURVEY.md Appendix B's known answer.
@@ -18,8 +18,9 @@ from __future__ import annotations
 import numpy as np
 
 
-def apply_factor_offset(x: np.ndarray, factor, offset=None) -> np.ndarray:
-    """functional.py:55-91 with clip_balanced=False: trunc((x + offset) / factor), clip [-128,127].
+def apply_factor_offset(x: np.ndarray, factor, offset=None, lo: int = -128) -> np.ndarray:
+    """functional.py:55-91: trunc((x + offset) / factor), clip to [lo, 127] (lo = -128:
+    clip_balanced=False; -127: clip_balanced=True, :89-91).
 
     ``x`` is [..., K, L] with the factor per K (second to last axis) or a scalar factor.
     Truncation toward zero is done with exact integer arithmetic (the reference divides in
@@ -35,7 +36,7 @@ def apply_factor_offset(x: np.ndarray, factor, offset=None) -> np.ndarray:
     num = x + offset
     q = np.abs(num) // np.abs(factor)
     q = np.where((num < 0) != (factor < 0), -q, q)
-    return np.clip(q, -128, 127)
+    return np.clip(q, lo, 127)
 
 
 def relu(x: np.ndarray, threshold: np.ndarray) -> np.ndarray:
@@ -60,11 +61,16 @@ def xcorr_same(x: np.ndarray, w: np.ndarray, pad_start: int, pad_end: int) -> np
     return np.einsum("bklj,kj->bkl", win, np.asarray(w, np.int64), optimize=True)
 
 
+def _lo(p) -> int:
+    """GoldenModel(clip_balanced=...) (golden_model.py:43): the ParamSet's clip mode."""
+    return -127 if getattr(p, "clip_balanced", False) else -128
+
+
 def layer1(p, x: np.ndarray) -> np.ndarray:
     """Layer1.__call__ (golden_model.py:192-196): depthwise_conv_space + apply_factor_offset.
     x: [B, C, T] -> [B, F2, T]."""
     y = np.einsum("bct,fc->bft", x.astype(np.int64), p.w1().astype(np.int64), optimize=True)
-    return apply_factor_offset(y, p.l1_factor, p.l1_offset)
+    return apply_factor_offset(y, p.l1_factor, p.l1_offset, _lo(p))
 
 
 def layer2(p, y1: np.ndarray) -> np.ndarray:
@@ -74,16 +80,17 @@ def layer2(p, y1: np.ndarray) -> np.ndarray:
     if not getattr(p, "reorder_bn", True):
         # reorder_bn=False (golden_model.py:248-251): BN per element with factor//8, bias//8
         # (clip), relu at 0, sum-pool 8, // 8
-        y = apply_factor_offset(a, p.l2_factor.astype(np.int64) // 8, p.l2_offset.astype(np.int64) // 8)
+        y = apply_factor_offset(a, p.l2_factor.astype(np.int64) // 8, p.l2_offset.astype(np.int64) // 8,
+                                _lo(p))
         return pool(np.maximum(y, 0), 8) // 8
     thr = -(p.l2_offset.astype(np.int64) // 8)
-    return apply_factor_offset(pool(relu(a, thr), 8), p.l2_factor, p.l2_offset)
+    return apply_factor_offset(pool(relu(a, thr), 8), p.l2_factor, p.l2_offset, _lo(p))
 
 
 def layer3(p, y2: np.ndarray) -> np.ndarray:
     """Layer3.__call__ (golden_model.py:285-289): depthwise_conv_time (pad 7/8), factor only."""
     a = xcorr_same(y2, p.w3_torch(), 7, 8)
-    return apply_factor_offset(a, np.int64(p.l3_factor))
+    return apply_factor_offset(a, np.int64(p.l3_factor), lo=_lo(p))
 
 
 def layer4(p, y3: np.ndarray) -> np.ndarray:
@@ -94,10 +101,11 @@ def layer4(p, y3: np.ndarray) -> np.ndarray:
         # reorder_bn=False (golden_model.py:337-340).  NB: the golden model clips each element to
         # int8 before the ReLU, the reference C (layer4.c:113-118) does not; the two only differ
         # when an element exceeds 127 (tests/test_variants.py pins both behaviours).
-        y = apply_factor_offset(b, p.l4_factor.astype(np.int64) // 8, p.l4_offset.astype(np.int64) // 8)
+        y = apply_factor_offset(b, p.l4_factor.astype(np.int64) // 8, p.l4_offset.astype(np.int64) // 8,
+                                _lo(p))
         return pool(np.maximum(y, 0), 8) // 8
     thr = -(p.l4_offset.astype(np.int64) // 8)
-    return apply_factor_offset(pool(relu(b, thr), 8), p.l4_factor, p.l4_offset)
+    return apply_factor_offset(pool(relu(b, thr), 8), p.l4_factor, p.l4_offset, _lo(p))
 
 
 def layer5(p, y4: np.ndarray) -> np.ndarray:
@@ -106,7 +114,7 @@ def layer5(p, y4: np.ndarray) -> np.ndarray:
     z = y4.reshape(B, -1).astype(np.int64) @ p.w5_flat().astype(np.int64).T + p.l5_bias.astype(np.int64)
     q = np.abs(z) // abs(p.l5_factor)
     q = np.where((z < 0) != (p.l5_factor < 0), -q, q)
-    return np.clip(q, -128, 127)
+    return np.clip(q, _lo(p), 127)
 
 
 def forward(p, x: np.ndarray, return_all: bool = False):

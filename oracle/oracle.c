@@ -4,7 +4,8 @@
  * Serial C restatement of the reference's canonical integer forward pass.  Each function cites
  * the reference lines it follows (paths relative to /root/reference/edge-eegnet_wolf).
  * Arithmetic: int32 accumulators, C '/' (truncation toward zero), '>>' arithmetic shift,
- * clip to [-128, 127] (__CLIP_R(x, 127) of the PULP SDK, clip_balanced=False in the golden model).
+ * clip to [-128, 127] (__CLIP_R(x, 127) of the PULP SDK, clip_balanced=False in the golden model;
+ * or_params_t.clip_lo = -127 gives the golden model's clip_balanced=True).
  */
 #include "oracle.h"
 
@@ -19,7 +20,11 @@
 #define L3_PAD_START 7 /* gen_net_header.py:162 */
 #define L3_PAD_END 8   /* gen_net_header.py:163 */
 
-static inline int32_t clip8(int32_t v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+/* clip to [p->clip_lo, 127]: clip_lo = -128 is the C's __CLIP_R(x, 127); -127 is the golden
+ * model's clip_balanced=True (functional.py:89-91), which has no C build */
+static inline int32_t clipq(const or_params_t* p, int32_t v) {
+    return v < p->clip_lo ? p->clip_lo : (v > 127 ? 127 : v);
+}
 
 /* func_dotp (func/dotp.c:45 NO_SIMD variant): plain int8 dot product into int32 */
 static inline int32_t dotp(const int8_t* a, const int8_t* b, int len) {
@@ -38,7 +43,7 @@ void or_layer1(const or_params_t* p, const int8_t* x, int8_t* y1) {
         for (int t = 0; t < p->T; t++) {
             int32_t e = dotp(x + (size_t)t * p->C_ALIGN, w, p->C_ALIGN);
             e = (e + off) / fac;
-            y1[(size_t)f * p->T_ALIGN + t] = (int8_t)clip8(e);
+            y1[(size_t)f * p->T_ALIGN + t] = (int8_t)clipq(p, e);
         }
     }
 }
@@ -74,7 +79,7 @@ void or_layer2(const or_params_t* p, const int8_t* y1, int8_t* y2) {
                 }
                 sum = sum + off;
                 sum = sum / fac;
-                y2[(size_t)f * p->T8_ALIGN + u] = (int8_t)clip8(sum);
+                y2[(size_t)f * p->T8_ALIGN + u] = (int8_t)clipq(p, sum);
             }
         } else {
             /* layer2.c:139-210: factor and offset >> 3, func_xcorr_scale (xcorr.c:346 ->
@@ -83,11 +88,11 @@ void or_layer2(const or_params_t* p, const int8_t* y1, int8_t* y2) {
             for (int u = 0; u < p->T8; u++) {
                 int32_t sum = 0;
                 for (int k = 0; k < 8; k++) {
-                    int32_t v = clip8((*(it++) + off3) / fac3);
+                    int32_t v = clipq(p, (*(it++) + off3) / fac3);
                     sum += v > 0 ? v : 0;
                 }
                 sum = sum >> 3;
-                y2[(size_t)f * p->T8_ALIGN + u] = (int8_t)clip8(sum);
+                y2[(size_t)f * p->T8_ALIGN + u] = (int8_t)clipq(p, sum);
             }
         }
     }
@@ -111,7 +116,7 @@ void or_layer3(const or_params_t* p, const int8_t* y2, int8_t* y3) {
             int32_t acc = 0; /* offset argument is 0 (layer3.c:70) */
             for (int j = 0; j < L3_TAPS; j++) acc += (int32_t)row[i + j] * (int32_t)w[L3_TAPS - 1 - j];
             acc = acc / p->l3_factor;
-            y3[(size_t)f * p->T8_ALIGN + i] = (int8_t)clip8(acc);
+            y3[(size_t)f * p->T8_ALIGN + i] = (int8_t)clipq(p, acc);
         }
     }
     free(row);
@@ -158,7 +163,7 @@ void or_layer4(const or_params_t* p, const int8_t* y3t, int8_t* y4) {
             } else {
                 sum = sum >> 3;  /* layer4.c:130 */
             }
-            y4[(size_t)k * p->T64_ALIGN + v] = (int8_t)clip8(sum);
+            y4[(size_t)k * p->T64_ALIGN + v] = (int8_t)clipq(p, sum);
         }
     }
 }
@@ -176,7 +181,7 @@ void or_layer5(const or_params_t* p, const int8_t* y4, int8_t* out) {
     for (int n = 0; n < p->N; n++) {
         int32_t z = dotp(xin, p->l5_weight + (size_t)n * len, len) + (int32_t)p->l5_bias[n];
         z = z / p->l5_factor;
-        out[n] = (int8_t)clip8(z);
+        out[n] = (int8_t)clipq(p, z);
     }
     free(xin);
 }

@@ -49,6 +49,8 @@ typedef struct {
     const int8_t*  l5_bias;         /* [N] */
     const int8_t*  l5_weight;       /* [N][F2*T64_ALIGN] */
     int32_t        reorder_bn;      /* 1: -DREORDER_BN branches (canonical), 0: the plain ones */
+    int32_t        clip_lo;         /* lower clip bound: -128 (the C's __CLIP_R) or -127 (golden
+                                       model clip_balanced=True, functional.py:89-91) */
 } or_params_t;
 
 void or_layer1(const or_params_t* p, const int8_t* x, int8_t* y1);
