@@ -110,6 +110,13 @@ int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, fl
 int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, double scale, int device,
                            void* stream);
 
+/* The step after the path: cls[b] = index of the largest of the N int8 logits of trial b, the
+ * first one on ties (torch.max(pr_outs, dim=1) of the reference's accuracy meter,
+ * QuantLab/quantlab/BCI-CompIV-2a/edgeEEGNet/postprocess.py:6-8).  logits: DEVICE pointer [B][N]
+ * (as net_model_compute_batch writes it), cls: DEVICE pointer [B].  1 <= N <= 64.  Enqueued on
+ * `stream` (NULL = null stream), no host sync. */
+int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int device, void* stream);
+
 /* Device used by the single-trial API (default 0). */
 int net_set_device(int device);
 

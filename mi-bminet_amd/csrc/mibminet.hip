@@ -22,6 +22,7 @@
 #include "../../include/mibminet.h"
 #include "forward_wg.hpp"
 #include "quantize.hpp"
+#include "classify.hpp"
 
 using namespace mib;
 
@@ -536,6 +537,16 @@ int quantize_input(const F* x, int8_t* y, size_t B, int C, int T, F scale, int d
   return hip_err(hipGetLastError());
 }
 
+int argmax_batch(const int8_t* logits, int32_t* out, size_t B, int N, int device, void* stream) {
+  if ((!logits || !out) && B) return NET_ERR_INVALID;
+  if (N < 1 || N > cls::NMAX || device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
+  if (B == 0) return NET_OK;
+  DeviceGuard guard(device);
+  const unsigned grid = (unsigned)((B + cls::CTHREADS - 1) / cls::CTHREADS);
+  hipLaunchKernelGGL(cls::k_argmax, dim3(grid), dim3(cls::CTHREADS), 0, (hipStream_t)stream, logits, out, (int)B, N);
+  return hip_err(hipGetLastError());
+}
+
 }  // namespace
 
 // ================================ C ABI ======================================================
@@ -627,6 +638,10 @@ int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, fl
 
 int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, double scale, int device, void* stream) {
   return quantize_input<double>(x, y, B, C, T, scale, device, stream);
+}
+
+int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int device, void* stream) {
+  return argmax_batch(logits, cls, B, N, device, stream);
 }
 
 int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device) {

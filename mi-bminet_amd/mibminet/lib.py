@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "net_layer3_flip_inplace", "net_layer4", "net_layer5", "net_last_error", "net_params_load",
     "net_params_dims", "net_params_unload", "net_trial_stride", "net_model_compute_batch",
     "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
-    "net_version", "net_quantize_input_f32", "net_quantize_input_f64",
+    "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
 )
 
 
@@ -95,6 +95,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_quantize_input_f32.restype = i
     L.net_quantize_input_f64.argtypes = [vp, vp, sz, i, i, ctypes.c_double, i, vp]
     L.net_quantize_input_f64.restype = i
+    L.net_argmax_batch.argtypes = [vp, vp, sz, i, i, vp]
+    L.net_argmax_batch.restype = i
     _lib = L
     return L
 
@@ -264,3 +266,18 @@ def quantize_input_torch(x, scale: float, stream=None):
         _check(fn(x[lo:].data_ptr(), y[lo:].data_ptr(), n, C, T, scale, x.device.index or 0, s.cuda_stream),
                "net_quantize_input")
     return y
+
+
+def argmax_torch(logits, stream=None):
+    """Class per trial (net_argmax_batch): logits is a CUDA/HIP int8 tensor [B][N]; returns an int32
+    tensor [B] holding the first maximal index of each row (torch.max(dim=1)'s rule)."""
+    import torch
+
+    if logits.dtype != torch.int8 or not logits.is_cuda or not logits.is_contiguous() or logits.dim() != 2:
+        raise ValueError("logits must be a contiguous int8 device tensor [B][N]")
+    B, N = logits.shape
+    out = torch.empty((B,), dtype=torch.int32, device=logits.device)
+    s = torch.cuda.current_stream(logits.device) if stream is None else stream
+    _check(load().net_argmax_batch(logits.data_ptr(), out.data_ptr(), B, N, logits.device.index or 0, s.cuda_stream),
+           "net_argmax_batch")
+    return out
