@@ -26,11 +26,82 @@ static inline int32_t clipq(const or_params_t* p, int32_t v) {
     return v < p->clip_lo ? p->clip_lo : (v > 127 ? 127 : v);
 }
 
-/* func_dotp (func/dotp.c:45 NO_SIMD variant): plain int8 dot product into int32 */
-static inline int32_t dotp(const int8_t* a, const int8_t* b, int len) {
+static inline int32_t clip8(int32_t v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+
+/* ---- func primitives (src/cl/func/{dotp,xcorr,conv,transform,flip}.c) ------------------------
+ * Each is pinned by the reference's own func test (test/cl/func/<name>/testcase.py: NumPy
+ * expectations at the sizes listed there) in tests/test_oracle_func.py, and the layers below
+ * are built from them. */
+
+/* func_dotp (dotp.c:45, and the SIMD form :82): int8 dot product into int32 */
+int32_t or_func_dotp(const int8_t* a, const int8_t* b, unsigned len) {
     int32_t acc = 0;
-    for (int i = 0; i < len; i++) acc += (int32_t)a[i] * (int32_t)b[i];
+    for (unsigned i = 0; i < len; i++) acc += (int32_t)a[i] * (int32_t)b[i];
     return acc;
+}
+
+static inline int32_t dotp(const int8_t* a, const int8_t* b, int len) { return or_func_dotp(a, b, (unsigned)len); }
+
+/* The longer vector is the signal (xcorr.c:44-57, conv.c:67-80 swap a and b when a is shorter). */
+static void order_ab(const int8_t** a, unsigned* la, const int8_t** b, unsigned* lb) {
+    if (*la < *lb) {
+        const int8_t* t = *a; *a = *b; *b = t;
+        unsigned n = *la; *la = *lb; *lb = n;
+    }
+}
+
+/* func_xcorr (xcorr.c:44): valid cross-correlation, r[i] = sum_j a[i + j] * b[j], la - lb + 1 outputs */
+void or_func_xcorr(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t* r) {
+    order_ab(&a, &la, &b, &lb);
+    for (unsigned i = 0; i + lb <= la; i++) r[i] = or_func_dotp(a + i, b, lb);
+}
+
+/* func_xcorr_scale (xcorr.c:346): clip((xcorr + offset) / div) */
+void or_func_xcorr_scale(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t div, int32_t offset,
+                         int8_t* r) {
+    order_ab(&a, &la, &b, &lb);
+    for (unsigned i = 0; i + lb <= la; i++) r[i] = (int8_t)clip8((or_func_dotp(a + i, b, lb) + offset) / div);
+}
+
+static inline int32_t conv_at(const int8_t* a, const int8_t* b, unsigned lb, unsigned i) {
+    int32_t acc = 0;
+    for (unsigned j = 0; j < lb; j++) acc += (int32_t)a[i + j] * (int32_t)b[lb - 1 - j];
+    return acc;
+}
+
+/* func_conv (conv.c:67): valid true convolution, r[i] = sum_j a[i + j] * b[lb - 1 - j] */
+void or_func_conv(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t* r) {
+    order_ab(&a, &la, &b, &lb);
+    for (unsigned i = 0; i + lb <= la; i++) r[i] = conv_at(a, b, lb, i);
+}
+
+/* func_conv_scale (conv.c:105): acc = offset + conv; clip(acc / div) */
+void or_func_conv_scale(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t div, int32_t offset,
+                        int8_t* r) {
+    order_ab(&a, &la, &b, &lb);
+    for (unsigned i = 0; i + lb <= la; i++) r[i] = (int8_t)clip8((offset + conv_at(a, b, lb, i)) / div);
+}
+
+/* func_transform_32to8 (transform.c:47): r[k] = clip(in[k * stride] / div).  Writes whole
+ * 4-byte packs: a partial last pack is zero-filled (transform.c:95-121), so r holds
+ * ceil(len / 4) * 4 bytes. */
+void or_func_transform_32to8(const int32_t* in, unsigned len, int32_t div, unsigned stride, int8_t* r) {
+    for (unsigned k = 0; k < (len + 3) / 4 * 4; k++) r[k] = k < len ? (int8_t)clip8(in[(size_t)k * stride] / div) : 0;
+}
+
+/* func_transform_32to8_bias (transform.c:138): r[k] = clip((in[k * stride] + bias) / div), same packing */
+void or_func_transform_32to8_bias(const int32_t* in, unsigned len, int32_t div, int32_t bias, unsigned stride,
+                                  int8_t* r) {
+    for (unsigned k = 0; k < (len + 3) / 4 * 4; k++)
+        r[k] = k < len ? (int8_t)clip8((in[(size_t)k * stride] + bias) / div) : 0;
+}
+
+/* func_flip_2d_axis (flip.c:92): in [outer][align4(inner)] -> r [inner][align4(outer)], the
+ * alignment padding of each output row zero (flip.c:161-300 writes whole 4-byte parts). */
+void or_func_flip_2d_axis(const int8_t* in, unsigned outer, unsigned inner, int8_t* r) {
+    const unsigned ia = (inner + 3) / 4 * 4, oa = (outer + 3) / 4 * 4;
+    for (unsigned i = 0; i < inner; i++)
+        for (unsigned o = 0; o < oa; o++) r[(size_t)i * oa + o] = o < outer ? in[(size_t)o * ia + i] : 0;
 }
 
 /* Layer 1: layer1.c:53-101 (_net_layer1_kernel) — per filter, per time sample:
@@ -56,17 +127,13 @@ void or_layer2(const or_params_t* p, const int8_t* y1, int8_t* y2) {
     const int pad_len = p->T + L2_PAD_START + L2_PAD_END;
     int8_t* row = (int8_t*)calloc((size_t)pad_len, 1);
     int32_t* xc = (int32_t*)malloc(sizeof(int32_t) * (size_t)(pad_len - L2_TAPS + 1));
+    int8_t* xs = (int8_t*)malloc((size_t)(pad_len - L2_TAPS + 1));
     memset(y2, 0, (size_t)p->F2 * p->T8_ALIGN);
     for (int f = 0; f < p->F2; f++) {
         memset(row, 0, (size_t)pad_len);
         memcpy(row + L2_PAD_START, y1 + (size_t)f * p->T_ALIGN, (size_t)p->T);
         const int8_t* w = p->l2_weight_reverse + (size_t)f * L2_TAPS;
-        const int n_out = pad_len - L2_TAPS + 1; /* == T */
-        for (int i = 0; i < n_out; i++) {
-            int32_t acc = 0;
-            for (int j = 0; j < L2_TAPS; j++) acc += (int32_t)row[i + j] * (int32_t)w[j];
-            xc[i] = acc;
-        }
+        or_func_xcorr(row, (unsigned)pad_len, w, L2_TAPS, xc); /* pad_len - 63 == T outputs */
         const int32_t fac = p->l2_factor[f], off = p->l2_offset[f];
         const int32_t* it = xc;
         if (p->reorder_bn) {
@@ -85,10 +152,12 @@ void or_layer2(const or_params_t* p, const int8_t* y1, int8_t* y2) {
             /* layer2.c:139-210: factor and offset >> 3, func_xcorr_scale (xcorr.c:346 ->
              * transform.c:224: clip((x + offset) / factor) to int8), then sum of 8 ReLUs >> 3, clip */
             const int32_t fac3 = fac >> 3, off3 = off >> 3;
+            or_func_xcorr_scale(row, (unsigned)pad_len, w, L2_TAPS, fac3, off3, xs);
+            const int8_t* is = xs;
             for (int u = 0; u < p->T8; u++) {
                 int32_t sum = 0;
                 for (int k = 0; k < 8; k++) {
-                    int32_t v = clipq(p, (*(it++) + off3) / fac3);
+                    int32_t v = *(is++); /* the ReLU makes the lower clip bound irrelevant */
                     sum += v > 0 ? v : 0;
                 }
                 sum = sum >> 3;
@@ -96,6 +165,7 @@ void or_layer2(const or_params_t* p, const int8_t* y1, int8_t* y2) {
             }
         }
     }
+    free(xs);
     free(xc);
     free(row);
 }
@@ -111,13 +181,9 @@ void or_layer3(const or_params_t* p, const int8_t* y2, int8_t* y3) {
         memset(row, 0, (size_t)pad_len);
         memcpy(row + L3_PAD_START, y2 + (size_t)f * p->T8_ALIGN, (size_t)p->T8);
         const int8_t* w = p->l3_weight + (size_t)f * L3_TAPS;
-        const int n_out = pad_len - L3_TAPS + 1; /* == T8 */
-        for (int i = 0; i < n_out; i++) {
-            int32_t acc = 0; /* offset argument is 0 (layer3.c:70) */
-            for (int j = 0; j < L3_TAPS; j++) acc += (int32_t)row[i + j] * (int32_t)w[L3_TAPS - 1 - j];
-            acc = acc / p->l3_factor;
-            y3[(size_t)f * p->T8_ALIGN + i] = (int8_t)clipq(p, acc);
-        }
+        int8_t* out = y3 + (size_t)f * p->T8_ALIGN;
+        or_func_conv_scale(row, (unsigned)pad_len, w, L3_TAPS, p->l3_factor, 0, out); /* offset 0: layer3.c:70 */
+        for (int i = 0; i < p->T8; i++) out[i] = (int8_t)clipq(p, out[i]);  /* balanced clipping */
     }
     free(row);
 }
@@ -128,8 +194,7 @@ void or_layer3_flip_inplace(const or_params_t* p, int8_t* y3) {
     int8_t* tmp = (int8_t*)malloc((size_t)p->F2 * p->T8_ALIGN);
     memcpy(tmp, y3, (size_t)p->F2 * p->T8_ALIGN);
     memset(y3, 0, (size_t)p->F2 * p->T8_ALIGN);
-    for (int f = 0; f < p->F2; f++)
-        for (int u = 0; u < p->T8; u++) y3[(size_t)u * p->F2 + f] = tmp[(size_t)f * p->T8_ALIGN + u];
+    or_func_flip_2d_axis(tmp, (unsigned)p->F2, (unsigned)p->T8, y3); /* F2 = 16: rows of F2 bytes */
     free(tmp);
 }
 
@@ -178,11 +243,13 @@ void or_layer5(const or_params_t* p, const int8_t* y4, int8_t* out) {
     for (int k = 0; k < p->F2; k++)
         for (int v = 0; v < p->T64_ALIGN; v++)
             xin[k * p->T64_ALIGN + v] = v < p->T64 ? y4[(size_t)k * p->T64_ALIGN + v] : 0;
-    for (int n = 0; n < p->N; n++) {
-        int32_t z = dotp(xin, p->l5_weight + (size_t)n * len, len) + (int32_t)p->l5_bias[n];
-        z = z / p->l5_factor;
-        out[n] = (int8_t)clipq(p, z);
-    }
+    int32_t* z = (int32_t*)malloc(sizeof(int32_t) * (size_t)p->N);
+    int8_t* zq = (int8_t*)malloc((size_t)(p->N + 3) / 4 * 4);
+    for (int n = 0; n < p->N; n++) z[n] = dotp(xin, p->l5_weight + (size_t)n * len, len) + (int32_t)p->l5_bias[n];
+    or_func_transform_32to8(z, (unsigned)p->N, p->l5_factor, 1, zq);
+    for (int n = 0; n < p->N; n++) out[n] = (int8_t)clipq(p, zq[n]);
+    free(zq);
+    free(z);
     free(xin);
 }
 

@@ -53,6 +53,19 @@ typedef struct {
                                        model clip_balanced=True, functional.py:89-91) */
 } or_params_t;
 
+/* func primitives (src/cl/func/{dotp,xcorr,conv,transform,flip}.c), clip to [-128, 127] as the C's __CLIP_R */
+int32_t or_func_dotp(const int8_t* a, const int8_t* b, unsigned len);
+void or_func_xcorr(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t* r);
+void or_func_xcorr_scale(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t div, int32_t offset,
+                         int8_t* r);
+void or_func_conv(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t* r);
+void or_func_conv_scale(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t div, int32_t offset,
+                        int8_t* r);
+void or_func_transform_32to8(const int32_t* in, unsigned len, int32_t div, unsigned stride, int8_t* r);
+void or_func_transform_32to8_bias(const int32_t* in, unsigned len, int32_t div, int32_t bias, unsigned stride,
+                                  int8_t* r);
+void or_func_flip_2d_axis(const int8_t* in, unsigned outer, unsigned inner, int8_t* r);
+
 void or_layer1(const or_params_t* p, const int8_t* x, int8_t* y1);
 void or_layer2(const or_params_t* p, const int8_t* y1, int8_t* y2);
 void or_layer3(const or_params_t* p, const int8_t* y2, int8_t* y3);
