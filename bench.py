@@ -225,7 +225,7 @@ def main():
                        "grid": info["grid"], "threads": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_forward<Cfg<%d,%d>>" % (cfg["C"], cfg["T"]),
+                         "kernel": "k_forward<Cfg<%d,%d,RB=1,CB=0>>" % (cfg["C"], cfg["T"]),
                          "avg_kernel_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes_trial * B},
             "cpu_baseline": None,

@@ -65,7 +65,7 @@ def main():
     fk = med(fetch)
     wk = med(write)
     write_bytes = wk * 1024
-    tj = {"config": "b22", "batch": 65536, "kernel": "k_forward<Cfg<22,1125>>",
+    tj = {"config": "b22", "batch": 65536, "kernel": "k_forward<Cfg<22,1125,RB=1,CB=0>>",
           "fetch_size_kB_raw": fk, "write_size_kB": wk, "write_bytes": write_bytes,
           "alg_bytes_per_launch": (22 * 1125 + 4) * 65536}
     rq = glob.glob(f"{src}/pmc_rdreq/**/*counter_collection.csv", recursive=True)
