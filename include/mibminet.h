@@ -78,7 +78,9 @@ int net_last_error(void);
  * BN branches of layer2.c:139-210 / layer4.c:91-133.  Flag bit 1: clip every requantised output to
  * [-127, 127], the golden model's clip_balanced=True, functional.py:89-91; clear: [-128, 127] as
  * the C's __CLIP_R).  Other flag bits are rejected (NET_ERR_BLOB).  Validates, precomputes the gfx950 operand fragments and exact requantisation
- * reciprocals, and uploads lazily to each device on first use.  Replaces any previous set. */
+ * reciprocals, and uploads lazily to each device on first use.  Replaces any previous set.  Safe
+ * against launches in flight: a call already enqueued keeps the set it started with, and the
+ * first call on a device after a reload waits for that device's work before replacing its copy. */
 int net_params_load(const void* blob, size_t len);
 
 /* dims[0..6] = C, T, F1, F2, N, weight_bits, loaded(0/1). */

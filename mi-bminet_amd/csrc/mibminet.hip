@@ -423,6 +423,13 @@ int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
     if (e != hipSuccess) return hip_err(e);
   }
   if (ds.gen != s.gen) {
+    // Kernels of the previous generation may still run on any stream of this device (the async
+    // entry point does not wait for them) and read d_params: let them finish before it changes.
+    // No new launch can be enqueued meanwhile (ds.mu is held).  Reloads are rare.
+    if (ds.gen != 0) {
+      hipError_t e = hipDeviceSynchronize();
+      if (e != hipSuccess) return hip_err(e);
+    }
     hipError_t e = hipMemcpy(ds.d_params, s.dev.get(), sizeof(DevParams), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_err(e);
     ds.gen = s.gen;
