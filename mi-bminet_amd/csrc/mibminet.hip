@@ -387,7 +387,7 @@ std::shared_ptr<const HostParams> g_host;
 std::shared_ptr<const DevParams> g_dev;
 uint64_t g_gen = 0;
 DeviceState g_devs[MAX_DEVICES];
-int g_single_device = 0;
+std::atomic<int> g_single_device{0};  // net_set_device (read by every single-trial call)
 thread_local int t_last_error = NET_OK;
 
 inline int hip_err(hipError_t e) { return e == hipSuccess ? NET_OK : NET_ERR_HIP - (int)e; }
@@ -492,7 +492,7 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
   const Dims& d = s.host->d;
   const Variant v = variant_of(*s.host);
   if (!v.ok()) return NET_ERR_UNSUPPORTED;
-  const int dev = g_single_device;
+  const int dev = g_single_device.load();
   DeviceState& ds = g_devs[dev];
   std::lock_guard<std::mutex> lk(ds.mu);
   DeviceGuard guard(dev);
@@ -619,7 +619,7 @@ int net_set_device(int device) {
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess) return hip_err(e);
   if (device < 0 || device >= n || device >= MAX_DEVICES) return NET_ERR_INVALID;
-  g_single_device = device;
+  g_single_device.store(device);
   return NET_OK;
 }
 
