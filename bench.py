@@ -92,9 +92,17 @@ def cpu_baseline(ps, x_dev, seconds):
                 break
     except OSError:
         pass
+    # (i) one core as well, on a smaller bounded sample
+    n1 = int(max(8, min(x_dev.shape[0], seconds / 5 / (per_trial * threads))))
+    s1 = x_dev[:n1].cpu().numpy()
+    t1 = time.perf_counter()
+    co.batch(s1, nthreads=1)
+    d1 = time.perf_counter() - t1
     return {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
             "sample": f"{n} trials ({reps} pass(es) over the first {n // reps} trials) of the same synthetic batch, C restatement (oracle/oracle.c, -O3) "
-                      f"of net_model_compute, {threads} host threads on {cpu}, {dt:.1f} s"}
+                      f"of net_model_compute, {threads} host threads on {cpu}, {dt:.1f} s",
+            "one_core": {"value": n1 / d1, "unit": "trials/s", "sample": f"{n1} trials, 1 thread, {d1:.1f} s"},
+            "host_cpus": {"affinity": ncpu, "os_cpu_count": os.cpu_count()}}
 
 
 def pcie_inclusive(x, y, B, device, sp, stream, reps=5):
