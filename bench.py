@@ -70,7 +70,7 @@ def cpu_baseline(ps, x_dev, seconds):
         ncpu = os.cpu_count() or 1
     threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", ncpu)), ncpu, 16))
     co = oracle.COracle(ps)
-    calib = x_dev[: 4 * threads].cpu().numpy()
+    calib = x_dev[: 32 * threads].cpu().numpy()
     t0 = time.perf_counter()
     co.batch(calib, nthreads=threads)
     dt = max(time.perf_counter() - t0, 1e-6)
