@@ -119,6 +119,12 @@ int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, d
  * `stream` (NULL = null stream), no host sync. */
 int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int device, void* stream);
 
+/* Already-quantised int8 trials in channel-major [B][C][T] (the layout of the reference's
+ * input.npz, transposed by gen_input_header.py:74 on the host): the same GPU transpose into the
+ * batched [B][stride] layout, without the quantisation.  DEVICE pointers, B <= 65535 per call,
+ * C <= 64, enqueued on `stream`, no host sync. */
+int net_pack_trials_i8(const int8_t* x, int8_t* y, size_t B, int C, int T, int device, void* stream);
+
 /* Device used by the single-trial API (default 0). */
 int net_set_device(int device);
 

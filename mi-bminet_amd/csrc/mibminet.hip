@@ -647,6 +647,10 @@ int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, d
   return quantize_input<double>(x, y, B, C, T, scale, device, stream);
 }
 
+int net_pack_trials_i8(const int8_t* x, int8_t* y, size_t B, int C, int T, int device, void* stream) {
+  return quantize_input<int8_t>(x, y, B, C, T, (int8_t)1, device, stream);
+}
+
 int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int device, void* stream) {
   return argmax_batch(logits, cls, B, N, device, stream);
 }

@@ -40,6 +40,13 @@ __device__ __forceinline__ int quantize_one<double>(double x, double s) {
   return (int)__dmul_rn(q, 127.0);
 }
 
+// int8 EEG already quantised ([B][C][T], the layout of SURVEY §8(b)'s batched signature): the same
+// kernel is then only the transpose into the forward's [T][C] trial layout
+template <>
+__device__ __forceinline__ int quantize_one<int8_t>(int8_t x, int8_t) {
+  return x;
+}
+
 template <class F>
 __global__ __launch_bounds__(QTHREADS) void k_quantize(const F* __restrict__ x, int8_t* __restrict__ y,
                                                        int C, int T, int stride, F s) {

@@ -32,6 +32,7 @@ EXPORTED_SYMBOLS = (
     "net_params_dims", "net_params_unload", "net_trial_stride", "net_model_compute_batch",
     "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
+    "net_pack_trials_i8",
 )
 
 
@@ -95,6 +96,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_quantize_input_f32.restype = i
     L.net_quantize_input_f64.argtypes = [vp, vp, sz, i, i, ctypes.c_double, i, vp]
     L.net_quantize_input_f64.restype = i
+    L.net_pack_trials_i8.argtypes = [vp, vp, sz, i, i, i, vp]
+    L.net_pack_trials_i8.restype = i
     L.net_argmax_batch.argtypes = [vp, vp, sz, i, i, vp]
     L.net_argmax_batch.restype = i
     _lib = L
@@ -281,3 +284,21 @@ def argmax_torch(logits, stream=None):
     _check(load().net_argmax_batch(logits.data_ptr(), out.data_ptr(), B, N, logits.device.index or 0, s.cuda_stream),
            "net_argmax_batch")
     return out
+
+
+def pack_trials_torch(x, stream=None):
+    """net_pack_trials_i8: x is a CUDA/HIP int8 tensor [B][C][T] (channel-major); returns the
+    batched layout [B][stride] (each trial [T][C], pad zero) that forward_torch consumes."""
+    import torch
+
+    if x.dtype != torch.int8 or not x.is_cuda or not x.is_contiguous() or x.dim() != 3:
+        raise ValueError("x must be a contiguous int8 device tensor [B][C][T]")
+    B, C, T = x.shape
+    stride = (C * T + 15) // 16 * 16
+    y = torch.empty((B, stride), dtype=torch.int8, device=x.device)
+    s = torch.cuda.current_stream(x.device) if stream is None else stream
+    for lo in range(0, B, 65535):
+        n = min(65535, B - lo)
+        _check(load().net_pack_trials_i8(x[lo:].data_ptr(), y[lo:].data_ptr(), n, C, T, x.device.index or 0,
+                                         s.cuda_stream), "net_pack_trials_i8")
+    return y

@@ -87,3 +87,44 @@ def test_gpu_float_input_path_end_to_end(gpu):
     y = lib.forward_torch(xq).cpu().numpy()
     want = oracle.COracle(ps).batch(G.quantize_input(x, 1.1), nthreads=4)
     assert np.array_equal(y, want)
+
+
+def test_pack_abi_checks():
+    from mibminet import lib
+
+    L = lib.load()
+    assert L.net_pack_trials_i8(None, None, 0, 22, 1125, 0, None) == 0  # empty batch
+    assert L.net_pack_trials_i8(None, None, 1, 22, 1125, 0, None) == lib.NET_ERR_INVALID
+    buf = np.zeros(64, np.int8)
+    assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 1, 65, 10, 0, None) == lib.NET_ERR_INVALID
+    assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 65536, 22, 1125, 0, None) == lib.NET_ERR_INVALID
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,T,B", [(22, 1125, 300), (64, 1000, 70), (5, 70, 33), (3, 1, 2)])
+def test_gpu_pack_trials_i8(gpu, C, T, B):
+    """int8 [B][C][T] -> the batched [T][C] layout on the GPU == pack_trials (NumPy)."""
+    import torch
+    from mibminet import lib
+    from mibminet.params import pack_trials
+
+    rng = np.random.default_rng(C + T + B)
+    x = rng.integers(-128, 128, size=(B, C, T)).astype(np.int8)
+    got = lib.pack_trials_torch(torch.from_numpy(x).to("cuda:0")).cpu().numpy()
+    assert np.array_equal(got, pack_trials(x))
+
+
+@pytest.mark.gpu
+def test_gpu_int8_channel_major_end_to_end(gpu):
+    """int8 [B][C][T] -> GPU pack -> fused forward == oracle."""
+    import torch
+    import oracle
+    from mibminet import lib
+    from mibminet.params import ParamSet, pack_trials
+
+    ps = ParamSet.synthetic(seed=12)
+    lib.params_load(ps)
+    rng = np.random.default_rng(6)
+    x = rng.integers(-128, 128, size=(257, 22, 1125)).astype(np.int8)
+    y = lib.forward_torch(lib.pack_trials_torch(torch.from_numpy(x).to("cuda:0"))).cpu().numpy()
+    assert np.array_equal(y, oracle.COracle(ps).batch(pack_trials(x), nthreads=4))
