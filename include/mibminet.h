@@ -100,6 +100,14 @@ int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device);
 /* Same, enqueued on `stream` (a hipStream_t of `device`, NULL = null stream), no host sync. */
 int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream);
 
+/* Several devices from one host thread (static split, no collectives): shard i is
+ * x[i] / y[i] / B[i] on devices[i] (DEVICE pointers of that device).  Every shard is enqueued
+ * before any is waited for, so the devices run concurrently.  streams == NULL: each device's null
+ * stream, and the call returns when all shards are done; otherwise streams[i] (a hipStream_t of
+ * devices[i]) and no host sync.  Returns the first error. */
+int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y,
+                                  const size_t* B, void* const* streams);
+
 /* Input quantiser / transposer (the step before the path; reference
  * edge-eegnet_wolf/data/gen_input_header.py:66-76 with python_utils/functional.py:308-334):
  * x: DEVICE pointer to B float trials [B][C][T]; y: DEVICE pointer to the batched int8 layout

@@ -655,6 +655,24 @@ int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int de
   return argmax_batch(logits, cls, B, N, device, stream);
 }
 
+int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y,
+                                  const size_t* B, void* const* streams) {
+  if (ndev < 1 || ndev > MAX_DEVICES || !devices || !x || !y || !B) return NET_ERR_INVALID;
+  // enqueue every shard first (launches are asynchronous), then wait: one host thread keeps all
+  // devices busy at once
+  for (int i = 0; i < ndev; i++) {
+    const int rc = net_model_compute_batch_async(x[i], y[i], B[i], devices[i], streams ? streams[i] : nullptr);
+    if (rc) return rc;
+  }
+  if (streams) return NET_OK;
+  for (int i = 0; i < ndev; i++) {
+    DeviceGuard guard(devices[i]);
+    const hipError_t e = hipStreamSynchronize(nullptr);
+    if (e != hipSuccess) return hip_err(e);
+  }
+  return NET_OK;
+}
+
 int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device) {
   int rc = net_model_compute_batch_async(x, y, B, device, nullptr);
   if (rc) return rc;

@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "net_params_dims", "net_params_unload", "net_trial_stride", "net_model_compute_batch",
     "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
-    "net_pack_trials_i8",
+    "net_pack_trials_i8", "net_model_compute_batch_multi",
 )
 
 
@@ -96,6 +96,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_quantize_input_f32.restype = i
     L.net_quantize_input_f64.argtypes = [vp, vp, sz, i, i, ctypes.c_double, i, vp]
     L.net_quantize_input_f64.restype = i
+    L.net_model_compute_batch_multi.argtypes = [i, vp, vp, vp, vp, vp]
+    L.net_model_compute_batch_multi.restype = i
     L.net_pack_trials_i8.argtypes = [vp, vp, sz, i, i, i, vp]
     L.net_pack_trials_i8.restype = i
     L.net_argmax_batch.argtypes = [vp, vp, sz, i, i, vp]
@@ -302,3 +304,16 @@ def pack_trials_torch(x, stream=None):
         _check(load().net_pack_trials_i8(x[lo:].data_ptr(), y[lo:].data_ptr(), n, C, T, x.device.index or 0,
                                          s.cuda_stream), "net_pack_trials_i8")
     return y
+
+
+def model_compute_batch_multi(xs, ys, devices) -> None:
+    """net_model_compute_batch_multi: xs[i] / ys[i] are device tensors on devices[i]
+    ([B_i][trial_stride] and [B_i][N] int8); one host call runs every shard and waits for all."""
+    n = len(devices)
+    if not (len(xs) == len(ys) == n):
+        raise ValueError("xs, ys and devices must have the same length")
+    dev = (ctypes.c_int * n)(*devices)
+    xp = (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])
+    yp = (ctypes.c_void_p * n)(*[y.data_ptr() for y in ys])
+    bs = (ctypes.c_size_t * n)(*[x.shape[0] for x in xs])
+    _check(load().net_model_compute_batch_multi(n, dev, xp, yp, bs, None), "net_model_compute_batch_multi")

@@ -8,6 +8,10 @@ the [B][N] logits after the fact.  There is no collective on the data path.
 One process per GPU (torch.distributed.run): ``shard_bounds`` picks the rank's slice,
 ``forward_shard`` runs it through the C ABI on the rank's device, ``gather_logits`` collects the
 shards on every rank (used by tests and tools, never inside a timed region).
+
+One process for all GPUs (one host thread driving every device):
+``forward_devices`` splits the batch the same way and runs all shards with one
+``net_model_compute_batch_multi`` call.
 """
 from __future__ import annotations
 
@@ -65,3 +69,27 @@ def gather_logits(y_shard: np.ndarray, batch: int, world: int, n_out: int = 4) -
         lo, hi = shard_bounds(batch, world, r)
         parts.append(outs[r].cpu().numpy()[: hi - lo].astype(np.int8))
     return np.concatenate(parts, axis=0)
+
+
+def forward_devices(x_global, devices):
+    """Logits of the whole batch ``x_global`` ([B][trial_stride] int8, host array or tensor) split
+    over ``devices`` with ``shard_bounds``: each shard is copied to its device, every device runs
+    concurrently from this one host thread (net_model_compute_batch_multi), and the [B][N] logits
+    come back concatenated in trial order."""
+    import torch
+    from . import lib
+
+    world = len(devices)
+    xs, ys = [], []
+    n_out = lib._dims().N
+    for r, d in enumerate(devices):
+        lo, hi = shard_bounds(x_global.shape[0], world, r)
+        part = x_global[lo:hi]
+        dev = torch.device("cuda", d)
+        xt = part.to(dev) if isinstance(part, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(part)).to(dev)
+        xs.append(xt.contiguous())
+        ys.append(torch.empty((hi - lo, n_out), dtype=torch.int8, device=dev))
+    for d in set(devices):
+        torch.cuda.synchronize(d)  # the copies above ran on torch's streams
+    lib.model_compute_batch_multi(xs, ys, list(devices))
+    return np.concatenate([y.cpu().numpy() for y in ys], axis=0)

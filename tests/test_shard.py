@@ -71,3 +71,29 @@ def test_gloo_world2_static_split(tmp_path, batch):
     for r in range(world):
         got = np.load(tmp_path / f"rank{r}.npy")
         assert np.array_equal(got, want)
+
+
+def test_multi_abi_checks():
+    from mibminet import lib
+
+    L = lib.load()
+    assert L.net_model_compute_batch_multi(0, None, None, None, None, None) == lib.NET_ERR_INVALID
+    assert L.net_model_compute_batch_multi(1, None, None, None, None, None) == lib.NET_ERR_INVALID
+    assert L.net_model_compute_batch_multi(99, None, None, None, None, None) == lib.NET_ERR_INVALID
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices,B", [([0], 1000), ([0, 0], 1001), ([0, 0, 0], 515)])
+def test_gpu_forward_devices(gpu, devices, B):
+    """One host thread, several shards (the same device listed several times stands in for the
+    8-GPU node here): the concatenated logits equal the oracle's for the whole batch."""
+    import oracle
+    from mibminet import lib
+    from mibminet.params import ParamSet, pack_trials
+    from mibminet.shard import forward_devices
+
+    ps = ParamSet.synthetic(seed=61)
+    lib.params_load(ps)
+    rng = np.random.default_rng(B)
+    x = pack_trials(rng.integers(-128, 128, size=(B, 22, 1125)))
+    assert np.array_equal(forward_devices(x, devices), oracle.COracle(ps).batch(x, nthreads=8))
