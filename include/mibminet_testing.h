@@ -1,0 +1,27 @@
+/*
+ * mibminet_testing.h — test hooks of libmibminet (not part of the reference's interface).
+ *
+ * The library turns every C truncating division of the path, y = clip(trunc(v / fac)), into a
+ * float multiply by a reciprocal r that it chooses and verifies on the host (DESIGN.md §3,
+ * "Exact requantisation").  This hook exposes that choice so the tests can check it against
+ * exhaustive integer division on the CPU.
+ */
+#ifndef MIBMINET_TESTING_H
+#define MIBMINET_TESTING_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The reciprocal the library would use for factor `fac` when |v| <= vmax and outputs must be
+ * exact up to step kmax (128 for int8 clipping).  magic != 0 also requires and returns
+ * c = -1.5 * 2^23 * r exact (the layer-1/3 fma form).  Returns 0, or NET_ERR_RANGE when no
+ * float reciprocal is exact over that range. */
+int mibminet_test_reciprocal(int32_t fac, int64_t vmax, int32_t kmax, int32_t magic, float* r, float* c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/mibminet.h"
+#include "../../include/mibminet_testing.h"
 #include "forward_wg.hpp"
 #include "quantize.hpp"
 #include "classify.hpp"
@@ -57,9 +58,11 @@ struct HostParams {
 // y = clip(trunc(v / fac), -128, 127) is computed on the GPU as clip((int)((float)v * r)).
 // (float)v is exact for |v| < 2^24 and (int) truncates toward zero.  q(v) = (int)RN(v * r) is
 // monotone in v, so it equals trunc(v / fac) on a whole constant interval of trunc(v / fac) iff it
-// does at both ends.  verify() checks both ends of the intervals for k = -129 .. 128, which pins
-// the clipped result for every v.  choose_reciprocal() starts at |1/fac| * (1 + 2^-22) (so that
-// exact multiples never round below the step) and nudges upward until verify() passes.
+// does at both ends.  verify() checks both ends of the intervals for k = -129 .. 128 that hold a
+// reachable v (|v| <= vmax, the layer's accumulator bound), which pins the clipped result for
+// every reachable v.  choose_reciprocal() starts two floats below RN(1/|fac|) and nudges upward
+// until verify() passes: for large factors the admissible window is only a few floats wide
+// (about 1 / (|fac| * 129) relative), so it must not be stepped over.
 
 inline int64_t trunc_div(int64_t a, int64_t b) { return a / b; }  // C semantics
 
@@ -97,9 +100,7 @@ bool choose_reciprocal(int32_t fac, float* out, float* magic_c = nullptr, int64_
   // fma(bits_as_float(v + 0x4B400000), r, c) == RN(v * r) (layer 1's one-instruction requant).
   if (fac == 0) return false;
   const double F = std::fabs((double)fac);
-  const double target = (1.0 / F) * (1.0 + std::ldexp(1.0, -22));
-  float r = (float)target;
-  if ((double)r < target) r = std::nextafterf(r, INFINITY);
+  float r = std::nextafterf(std::nextafterf((float)(1.0 / F), 0.0f), 0.0f);
   for (int tries = 0; tries < 4096; tries++) {
     const float rs = fac < 0 ? -r : r;
     bool ok = true;
@@ -240,7 +241,8 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     for (int j = 0; j < 16; j++) {
       const int f = P == 2 ? 8 * t + (j >> 1) : j;
       dp.l1_cinit[t][j] = hp.l1_offset[f] + FMAGIC_I;
-      if (!choose_reciprocal(hp.l1_factor[f], &dp.l1_r[t][j], &dp.l1_c[t][j])) return NET_ERR_RANGE;
+      const int64_t v1 = (int64_t)C * A + std::llabs((int64_t)hp.l1_offset[f]);  // |dot + off|
+      if (!choose_reciprocal(hp.l1_factor[f], &dp.l1_r[t][j], &dp.l1_c[t][j], 128, v1)) return NET_ERR_RANGE;
     }
   }
   // layer 2: A operand = banded weights; row i <-> shift n(i) so that lane (c, h) register r
@@ -263,7 +265,9 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
       }
     dp.l2_thr[f] = -(hp.l2_offset[f] >> 3);
     dp.l2_off[f] = hp.l2_offset[f];
-    if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f])) return NET_ERR_RANGE;
+    // pooled sum + offset lies in [0, 8 * 64 * A + |off|] (8 * (off >> 3) <= off)
+    const int64_t v2 = 8LL * 64 * A + std::llabs((int64_t)hp.l2_offset[f]);
+    if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f], nullptr, 128, v2)) return NET_ERR_RANGE;
     dp.sp.l2_thr[f] = dp.l2_thr[f];
     dp.sp.l2_off[f] = dp.l2_off[f];
     dp.sp.l2_r[f] = dp.l2_r[f];
@@ -306,7 +310,7 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     }
   }
   // |layer-3 accumulator| <= 16 * 128 * 128 < 2^22: magic C-init form
-  if (!choose_reciprocal(hp.l3_factor, &sp.l3_r, &sp.l3_c)) return NET_ERR_RANGE;
+  if (!choose_reciprocal(hp.l3_factor, &sp.l3_r, &sp.l3_c, 128, 16LL * A)) return NET_ERR_RANGE;
   // layer 4: B operand of MFMA 32x32x32 = W4^T, block diagonal: lane (column k, half h) holds
   // K-slots 16h..16h+15; columns 0..15 carry output channels 0..15 on slots 0..15 and columns
   // 16..31 repeat them on slots 16..31 (a second 32-sample time block rides in the other K half).
@@ -319,7 +323,8 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
   for (int k = 0; k < F2; k++) {
     sp.l4_thr[k] = -(hp.l4_offset[k] >> 3);
     sp.l4_off[k] = hp.l4_offset[k];
-    if (!choose_reciprocal(hp.l4_factor[k], &sp.l4_r[k])) return NET_ERR_RANGE;
+    const int64_t v4 = 8LL * F2 * A + std::llabs((int64_t)hp.l4_offset[k]);
+    if (!choose_reciprocal(hp.l4_factor[k], &sp.l4_r[k], nullptr, 128, v4)) return NET_ERR_RANGE;
   }
   const int T64 = d.T64(), T64A = d.T64_ALIGN();
   if (F2 * T64A / 4 > ND5_MAX) return NET_ERR_UNSUPPORTED;
@@ -329,7 +334,7 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
       for (int v = 0; v < T64; v++) dst[k * T64A + v] = hp.l5_weight[(size_t)n * F2 * T64A + k * T64A + v];
     sp.l5_b[n] = hp.l5_bias[n];
   }
-  if (!choose_reciprocal(hp.l5_factor, &sp.l5_r)) return NET_ERR_RANGE;
+  if (!choose_reciprocal(hp.l5_factor, &sp.l5_r, nullptr, 128, (int64_t)F2 * T64 * A + 128)) return NET_ERR_RANGE;
   return NET_OK;
 }
 
@@ -649,6 +654,11 @@ int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, d
 
 int net_pack_trials_i8(const int8_t* x, int8_t* y, size_t B, int C, int T, int device, void* stream) {
   return quantize_input<int8_t>(x, y, B, C, T, (int8_t)1, device, stream);
+}
+
+int mibminet_test_reciprocal(int32_t fac, int64_t vmax, int32_t kmax, int32_t magic, float* r, float* c) {
+  if (!r || (magic && !c) || vmax < 0 || vmax >= (1 << 24)) return NET_ERR_INVALID;
+  return choose_reciprocal(fac, r, magic ? c : nullptr, kmax, vmax) ? NET_OK : NET_ERR_RANGE;
 }
 
 int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int device, void* stream) {

@@ -82,3 +82,16 @@ def test_appendix_b_factors_accepted():
     net, cfg, _ = appendix_b_net(0)
     lib.params_load(ParamSet.from_quantlab(net, cfg))
     lib.params_unload()
+
+
+def test_envelope_bounds_exact():
+    """The requant envelope: offsets one below each bound load, at the bound fail."""
+    L = lib.load()
+    A = 128 * 128
+    for name, bound in (("l1", (1 << 22) - 22 * A), ("l2", (1 << 24) - 8 * 64 * A), ("l4", (1 << 24) - 8 * 16 * A)):
+        for off, rc in ((bound - 1, 0), (-(bound - 1), 0), (bound, lib.NET_ERR_RANGE), (-bound, lib.NET_ERR_RANGE)):
+            ps = ParamSet.synthetic(seed=2)
+            getattr(ps, f"{name}_offset")[5] = off
+            b = ps.to_blob()
+            assert L.net_params_load(b, len(b)) == rc, (name, off)
+    lib.params_unload()
