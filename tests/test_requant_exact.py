@@ -59,3 +59,8 @@ def test_small_vmax_uses_the_bound():
     """With a small reachable range even a huge factor has a reciprocal (everything maps to 0)."""
     rc, r, _ = _reciprocal(2**31 - 1, 16 * 128 * 128, False)
     assert rc == 0 and 0 < r < 1e-8
+
+
+@pytest.mark.parametrize("fac", [2**31 - 1, -2**31, 2**24 + 1, -(2**23) - 3])
+def test_int32_extremes(fac):
+    _check_exhaustive(fac, (1 << 22) - 1, True)
