@@ -34,6 +34,7 @@ CONFIGS = {
     "b22": dict(C=22, T=1125, wbits=8, name="B: 22ch x 1125 int8, 4-class"),
     "c64": dict(C=64, T=1000, wbits=8, name="C: 64ch x 1000 int8, 4-class"),
     "d22": dict(C=22, T=1125, wbits=4, name="D: 22ch x 1125, int4 weights / int8 acts"),
+    "p64": dict(C=64, T=480, wbits=8, name="PhysioNet MMMI: 64ch x 480 int8, 4-class (not a BASELINE config)"),
 }
 
 

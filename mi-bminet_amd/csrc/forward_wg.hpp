@@ -96,13 +96,18 @@ struct Cfg {
   static constexpr int NBW = cmax(SPL.cm + (SPL.rm ? 1 : 0), SPL.cl);  // L1 blocks per wave (max)
   static constexpr int PF = cmin(NBW, PF_MAX);          // of which prefetched a trial ahead
   static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
-  static constexpr int MT = NB2 / 32;                   // full L2 tiles per filter
-  static constexpr int TB = NB2 - 32 * MT;              // tail blocks (of 32 outputs) per filter
+  // full L2 tiles per filter, then a tail of TB blocks on the 16x16x64 chain when the wave's two
+  // filters' tail columns fit its 16 columns (FPW * TC <= 16); otherwise (short trials, e.g.
+  // T = 480) the last tile is a partial 32x32 tile whose columns past NB2 are computed and dropped
+  static constexpr int MT0 = NB2 / 32;
+  static constexpr bool TAIL = NB2 > 32 * MT0 && FPW * 2 * (NB2 - 32 * MT0) <= 16;
+  static constexpr int MT = (TAIL || NB2 == 32 * MT0) ? MT0 : MT0 + 1;
+  static constexpr int TB = TAIL ? NB2 - 32 * MT0 : 0;  // tail blocks (of 32 outputs) per filter
   static constexpr int TC = 2 * TB;                     // tail columns (of 16 outputs) per filter
   // layer-1 rows hold positions pos = t + 32 (32 leading zeros = the xcorr pad of 31, aligned).
   // P == 2: parity-split planes [pos & 1][pos >> 1]: each lane's 4 outputs (one parity) are
   // contiguous and layer 2's K-window slices are 16-B aligned.
-  static constexpr int NPOS = cmax(32 + 16 * P * NB1, 32 * (NB2 - 1) + 96);
+  static constexpr int NPOS = cmax(cmax(32 + 16 * P * NB1, 32 * (NB2 - 1) + 96), 1024 * MT + 64);
   static constexpr int PLANE = align16((NPOS + P - 1) / P);
   static constexpr int Y1ROW = P * PLANE;
   static constexpr int XTRIAL = align16(T * C);         // batched trial stride (bytes)

@@ -339,10 +339,11 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
 }
 
 // ---- compiled configurations --------------------------------------------------------------
-// Two shapes, 22 x 1125 (BCI-IV-2a: configs A, B, D, E) and 64 x 1000 (config C), each compiled
+// Three shapes: 22 x 1125 (BCI-IV-2a: configs A, B, D, E), 64 x 1000 (config C) and 64 x 480 (the
+// reference's PhysioNet MMMI edgeEEGNet, QuantLab/PhysionetMMMI/config_INQ.json), each compiled
 // with and without -DREORDER_BN and with both clip modes: wg::Cfg<C, T, RB, CB>.
 struct Variant {
-  int shape = -1;  // 0: 22 x 1125, 1: 64 x 1000, -1: unsupported
+  int shape = -1;  // 0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480, -1: unsupported
   bool rb = true;  // -DREORDER_BN branches (canonical)
   bool cb = false; // golden-model clip_balanced (clip to [-127, 127])
   bool ok() const { return shape >= 0; }
@@ -353,6 +354,7 @@ Variant variant_of(const HostParams& hp) {
   Variant v;
   if (d.C == 22 && d.T == 1125) v.shape = 0;
   else if (d.C == 64 && d.T == 1000) v.shape = 1;
+  else if (d.C == 64 && d.T == 480) v.shape = 2;
   v.rb = hp.reorder_bn;
   v.cb = hp.clip_balanced;
   return v;
@@ -370,6 +372,7 @@ int dispatch(const Variant& v, F&& f) {
   switch (v.shape) {
     case 0: return with_variant<22, 1125>(v, f);
     case 1: return with_variant<64, 1000>(v, f);
+    case 2: return with_variant<64, 480>(v, f);
     default: return NET_ERR_UNSUPPORTED;
   }
 }
