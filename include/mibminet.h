@@ -78,9 +78,13 @@ int net_last_error(void);
  * BN branches of layer2.c:139-210 / layer4.c:91-133.  Flag bit 1: clip every requantised output to
  * [-127, 127], the golden model's clip_balanced=True, functional.py:89-91; clear: [-128, 127] as
  * the C's __CLIP_R).  Other flag bits are rejected (NET_ERR_BLOB).  Validates, precomputes the gfx950 operand fragments and exact requantisation
- * reciprocals, and uploads lazily to each device on first use.  Replaces any previous set.  Safe
- * against launches in flight: a call already enqueued keeps the set it started with, and the
- * first call on a device after a reload waits for that device's work before replacing its copy. */
+ * reciprocals, and uploads lazily to each device on first use.  Replaces any previous set.  Pad
+ * bytes of net_l1_weight_align (channels C..C_ALIGN-1) and of net_l5_weight (columns
+ * T64..T64_ALIGN-1 of every row) must be zero, as gen_net_header.py writes them (NET_ERR_BLOB
+ * otherwise).  Each distinct set gets its own device copy, which is never overwritten and is kept
+ * until the process exits (about 72 KB per set and device): launches already enqueued, and
+ * launches captured into a HIP graph, keep running the set (and build variant) they were
+ * enqueued with, whatever is loaded later. */
 int net_params_load(const void* blob, size_t len);
 
 /* dims[0..6] = C, T, F1, F2, N, weight_bits, loaded(0/1). */
@@ -94,7 +98,8 @@ void net_params_unload(void);
 size_t net_trial_stride(void);
 
 /* Forward B trials resident on `device`; x: device pointer [B][trial_stride], y: device pointer
- * [B][N].  Launches on the device's null stream and waits for completion. */
+ * [B][N].  x must be 16-byte aligned and y 4-byte aligned (NET_ERR_INVALID otherwise; hipMalloc
+ * and torch allocations are).  Launches on the device's null stream and waits for completion. */
 int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device);
 
 /* Same, enqueued on `stream` (a hipStream_t of `device`, NULL = null stream), no host sync. */
@@ -104,7 +109,8 @@ int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int devi
  * x[i] / y[i] / B[i] on devices[i] (DEVICE pointers of that device).  Every shard is enqueued
  * before any is waited for, so the devices run concurrently.  streams == NULL: each device's null
  * stream, and the call returns when all shards are done; otherwise streams[i] (a hipStream_t of
- * devices[i]) and no host sync.  Returns the first error. */
+ * devices[i]) and no host sync.  Returns the first error; the shards enqueued before it have
+ * finished by then (in both modes). */
 int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y,
                                   const size_t* B, void* const* streams);
 

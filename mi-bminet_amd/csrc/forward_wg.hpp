@@ -759,6 +759,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   const SmallParams* sp = (const SmallParams*)(smem + K::OFF_SP);
   if ((int)blockIdx.x < B)
     prefetch_l1<K>(trial_rsrc<K>(x + MIB_TRIAL_OFF(blockIdx.x), MIB_TRIALS_LEFT(blockIdx.x), wave), R);
+  // The first trial's fragments land before its layer 1 starts, as in k_layer (where loads still
+  // in flight at layer 1 gave a rare wrong layer-1 row).  Once per workgroup.
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   MIB_STAMP_INIT
   // Per trial two barriers: A after layer 1 (layer 2 of a filter reads all waves' layer-1

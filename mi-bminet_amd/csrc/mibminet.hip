@@ -189,6 +189,16 @@ int parse_blob(const void* blob, size_t len, HostParams& hp) {
   hp.l5_bias = r.i8(d.N);
   hp.l5_weight = r.w((size_t)d.N * F2 * d.T64_ALIGN(), d.wbits);
   if (!r.ok || r.pos != len) return NET_ERR_BLOB;
+  // The reference multiplies these pads too (func_dotp over all C_ALIGN / F2 * T64_ALIGN bytes,
+  // layer1.c:90, layer5.c:81) and gen_net_header.py writes them as zeros; the GPU skips them, so
+  // a blob with non-zero pads is rejected, as ParamSet.validate does.
+  for (int f = 0; f < F2; f++)
+    for (int c = d.C; c < d.C_ALIGN(); c++)
+      if (hp.l1_weight_align[(size_t)f * d.C_ALIGN() + c] != 0) return NET_ERR_BLOB;
+  for (int n = 0; n < d.N; n++)
+    for (int k = 0; k < F2; k++)
+      for (int v = d.T64(); v < d.T64_ALIGN(); v++)
+        if (hp.l5_weight[((size_t)n * F2 + k) * d.T64_ALIGN() + v] != 0) return NET_ERR_BLOB;
   return NET_OK;
 }
 
@@ -380,11 +390,21 @@ int dispatch(const Variant& v, F&& f) {
 size_t trial_stride(const Dims& d) { return ((size_t)d.C * d.T + 15) / 16 * 16; }
 
 // ---- global state --------------------------------------------------------------------------
+// One device copy of the parameter image per loaded generation: a load never overwrites a copy
+// that a kernel may still read, so launches in flight and launches captured into a HIP graph keep
+// the image (and with it the compiled variant) they were enqueued with.  Copies are released only
+// at process exit; a reload of a byte-identical image reuses its copy.
+struct DevImage {
+  std::shared_ptr<const DevParams> host;  // what was uploaded
+  DevParams* dev = nullptr;
+};
+
 struct DeviceState {
   std::mutex mu;
-  uint64_t gen = 0;           // params generation uploaded
-  DevParams* d_params = nullptr;
-  int8_t* d_in = nullptr;     // single-trial scratch
+  uint64_t gen = 0;             // params generation of `cur`
+  DevParams* cur = nullptr;     // device copy of that generation
+  std::vector<DevImage> images; // every copy uploaded to this device
+  int8_t* d_in = nullptr;       // single-trial scratch
   int8_t* d_out = nullptr;
   size_t scratch = 0;
   int cus = 0;
@@ -396,13 +416,29 @@ std::shared_ptr<const DevParams> g_dev;
 uint64_t g_gen = 0;
 DeviceState g_devs[MAX_DEVICES];
 std::atomic<int> g_single_device{0};  // net_set_device (read by every single-trial call)
+std::atomic<int> g_device_count{-1};
 thread_local int t_last_error = NET_OK;
 
 inline int hip_err(hipError_t e) { return e == hipSuccess ? NET_OK : NET_ERR_HIP - (int)e; }
 
-struct DeviceGuard {  // restores the caller's current device
+// NET_OK if `device` names a visible HIP device, NET_ERR_INVALID otherwise (or the HIP error).
+int check_device(int device) {
+  int n = g_device_count.load();
+  if (n < 0) {
+    const hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) return hip_err(e);
+    g_device_count.store(n);
+  }
+  return (device >= 0 && device < n && device < MAX_DEVICES) ? NET_OK : NET_ERR_INVALID;
+}
+
+struct DeviceGuard {  // makes `dev` current and restores the caller's device; err: hipSetDevice's status
   int old = -1;
-  explicit DeviceGuard(int dev) { if (hipGetDevice(&old) != hipSuccess) old = -1; (void)hipSetDevice(dev); }
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&old) != hipSuccess) old = -1;
+    err = hipSetDevice(dev);
+  }
   ~DeviceGuard() { if (old >= 0) (void)hipSetDevice(old); }
 };
 
@@ -417,7 +453,7 @@ Snapshot snapshot() {
   return Snapshot{g_host, g_dev, g_gen};
 }
 
-// Ensure `dev` holds the current parameters; called with ds.mu held and the device current.
+// Ensure `dev` holds the current parameters (ds.cur); called with ds.mu held and the device current.
 int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
   if (!s.host) return NET_ERR_NO_PARAMS;
   if (ds.cus == 0) {
@@ -426,20 +462,24 @@ int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
     if (e != hipSuccess) return hip_err(e);
     ds.cus = cus;
   }
-  if (!ds.d_params) {
-    hipError_t e = hipMalloc((void**)&ds.d_params, sizeof(DevParams));
+  if (ds.gen != s.gen || !ds.cur) {
+    for (const DevImage& im : ds.images)  // a set loaded before: its copy is still there, unchanged
+      if (im.host == s.dev || std::memcmp(im.host.get(), s.dev.get(), sizeof(DevParams)) == 0) {
+        ds.cur = im.dev;
+        ds.gen = s.gen;
+        return NET_OK;
+      }
+    DevImage im;
+    im.host = s.dev;
+    hipError_t e = hipMalloc((void**)&im.dev, sizeof(DevParams));
     if (e != hipSuccess) return hip_err(e);
-  }
-  if (ds.gen != s.gen) {
-    // Kernels of the previous generation may still run on any stream of this device (the async
-    // entry point does not wait for them) and read d_params: let them finish before it changes.
-    // No new launch can be enqueued meanwhile (ds.mu is held).  Reloads are rare.
-    if (ds.gen != 0) {
-      hipError_t e = hipDeviceSynchronize();
-      if (e != hipSuccess) return hip_err(e);
+    e = hipMemcpy(im.dev, s.dev.get(), sizeof(DevParams), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(im.dev);
+      return hip_err(e);
     }
-    hipError_t e = hipMemcpy(ds.d_params, s.dev.get(), sizeof(DevParams), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_err(e);
+    ds.images.push_back(im);
+    ds.cur = im.dev;
     ds.gen = s.gen;
   }
   return NET_OK;
@@ -504,6 +544,7 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
   DeviceState& ds = g_devs[dev];
   std::lock_guard<std::mutex> lk(ds.mu);
   DeviceGuard guard(dev);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, dev, s);
   if (rc) return rc;
   const size_t xs = trial_stride(d);
@@ -531,9 +572,9 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
                            hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_err(e);
   if (stage == 0)
-    rc = launch_forward(v, ds, ds.d_params, ds.d_in, ds.d_out, 1, 0);
+    rc = launch_forward(v, ds, ds.cur, ds.d_in, ds.d_out, 1, 0);
   else
-    rc = launch_layer(v, ds.d_params, ds.d_in, ds.d_out, stage);
+    rc = launch_layer(v, ds.cur, ds.d_in, ds.d_out, stage);
   if (rc) return rc;
   e = hipMemcpy(out, ds.d_out, out_bytes, hipMemcpyDeviceToHost);
   return hip_err(e);
@@ -545,8 +586,10 @@ int quantize_input(const F* x, int8_t* y, size_t B, int C, int T, F scale, int d
   if (C < 1 || C > quant::CMAX || T < 1 || device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
   if (B > 65535 || !(scale > 0)) return NET_ERR_INVALID;
   if (B == 0) return NET_OK;
+  if (const int rc = check_device(device)) return rc;
   const int stride = (int)(((size_t)C * T + 15) / 16 * 16);
   DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
   dim3 grid((T + quant::TT - 1) / quant::TT, (unsigned)B);
   hipLaunchKernelGGL(quant::k_quantize<F>, grid, dim3(quant::QTHREADS), 0, (hipStream_t)stream, x, y, C, T, stride, scale);
   return hip_err(hipGetLastError());
@@ -556,7 +599,9 @@ int argmax_batch(const int8_t* logits, int32_t* out, size_t B, int N, int device
   if ((!logits || !out) && B) return NET_ERR_INVALID;
   if (N < 1 || N > cls::NMAX || device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
   if (B == 0) return NET_OK;
+  if (const int rc = check_device(device)) return rc;
   DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
   const unsigned grid = (unsigned)((B + cls::CTHREADS - 1) / cls::CTHREADS);
   hipLaunchKernelGGL(cls::k_argmax, dim3(grid), dim3(cls::CTHREADS), 0, (hipStream_t)stream, logits, out, (int)B, N);
   return hip_err(hipGetLastError());
@@ -623,10 +668,7 @@ size_t net_trial_stride(void) {
 }
 
 int net_set_device(int device) {
-  int n = 0;
-  hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess) return hip_err(e);
-  if (device < 0 || device >= n || device >= MAX_DEVICES) return NET_ERR_INVALID;
+  if (const int rc = check_device(device)) return rc;
   g_single_device.store(device);
   return NET_OK;
 }
@@ -639,12 +681,14 @@ int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int devi
   if (!s.host) return NET_ERR_NO_PARAMS;
   const Variant v = variant_of(*s.host);
   if (!v.ok()) return NET_ERR_UNSUPPORTED;
+  if (const int rc = check_device(device)) return rc;
   DeviceState& ds = g_devs[device];
   std::lock_guard<std::mutex> lk(ds.mu);
   DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
-  return launch_forward(v, ds, ds.d_params, x, y, B, (hipStream_t)stream);
+  return launch_forward(v, ds, ds.cur, x, y, B, (hipStream_t)stream);
 }
 
 int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, float scale, int device, void* stream) {
@@ -672,24 +716,34 @@ int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* co
                                   const size_t* B, void* const* streams) {
   if (ndev < 1 || ndev > MAX_DEVICES || !devices || !x || !y || !B) return NET_ERR_INVALID;
   // enqueue every shard first (launches are asynchronous), then wait: one host thread keeps all
-  // devices busy at once
+  // devices busy at once.  On an error the shards already enqueued are waited for before
+  // returning, so no kernel still writes a caller's buffer when the error reaches it.
+  auto wait = [&](int n) -> int {
+    int first = NET_OK;
+    for (int i = 0; i < n; i++) {
+      DeviceGuard guard(devices[i]);
+      hipError_t e = guard.err;
+      if (e == hipSuccess) e = hipStreamSynchronize(streams ? (hipStream_t)streams[i] : nullptr);
+      if (e != hipSuccess && first == NET_OK) first = hip_err(e);
+    }
+    return first;
+  };
   for (int i = 0; i < ndev; i++) {
     const int rc = net_model_compute_batch_async(x[i], y[i], B[i], devices[i], streams ? streams[i] : nullptr);
-    if (rc) return rc;
+    if (rc) {
+      (void)wait(i);
+      return rc;
+    }
   }
   if (streams) return NET_OK;
-  for (int i = 0; i < ndev; i++) {
-    DeviceGuard guard(devices[i]);
-    const hipError_t e = hipStreamSynchronize(nullptr);
-    if (e != hipSuccess) return hip_err(e);
-  }
-  return NET_OK;
+  return wait(ndev);
 }
 
 int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device) {
   int rc = net_model_compute_batch_async(x, y, B, device, nullptr);
   if (rc) return rc;
   DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
   return hip_err(hipStreamSynchronize(nullptr));
 }
 
@@ -698,9 +752,11 @@ int net_launch_info(size_t B, int device, int32_t* out) {
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
   const Variant v = variant_of(*s.host);
+  if (const int rc = check_device(device)) return rc;
   DeviceState& ds = g_devs[device];
   std::lock_guard<std::mutex> lk(ds.mu);
   DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
   return launch_forward(v, ds, nullptr, nullptr, nullptr, B, nullptr, out);

@@ -60,3 +60,38 @@ def test_graph_float_path(gpu):
     torch.cuda.synchronize()
     want = oracle.COracle(ps).batch(G.quantize_input(x, 1.3), nthreads=8)
     assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_graph_keeps_its_parameter_set(gpu):
+    """A graph captured under one parameter set keeps replaying that set's kernel variant and
+    weights after a load that switches both build flags (plain BN, balanced clipping) and every
+    weight: each set has its own device copy, which no later load overwrites."""
+    import torch
+
+    ps_a = ParamSet.synthetic(seed=53)
+    ps_b = ParamSet.synthetic(seed=54, reorder_bn=False, clip_balanced=True)
+    rng = np.random.default_rng(53)
+    x = pack_trials(rng.integers(-128, 128, size=(700, 22, 1125)))
+    want_a = oracle.COracle(ps_a).batch(x, nthreads=8)
+    want_b = oracle.COracle(ps_b).batch(x, nthreads=8)
+    assert not np.array_equal(want_a, want_b)
+    xin = torch.from_numpy(x).cuda()
+    lib.params_load(ps_a)
+    lib.forward_torch(xin)  # eager call: uploads set A
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            out_a = lib.forward_torch(xin, stream=s)
+    lib.params_load(ps_b)
+    eager_b = lib.forward_torch(xin)  # uploads set B to its own copy
+    torch.cuda.synchronize()
+    assert np.array_equal(eager_b.cpu().numpy(), want_b)
+    out_a.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out_a.cpu().numpy(), want_a)
+    # reloading A reuses its copy; the graph and eager calls agree again
+    lib.params_load(ps_a)
+    assert np.array_equal(lib.forward_torch(xin).cpu().numpy(), want_a)

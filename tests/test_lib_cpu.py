@@ -95,3 +95,25 @@ def test_envelope_bounds_exact():
             b = ps.to_blob()
             assert L.net_params_load(b, len(b)) == rc, (name, off)
     lib.params_unload()
+
+
+def test_params_load_rejects_nonzero_pads():
+    """Pad weights the reference multiplies (func_dotp over C_ALIGN and F2 * T64_ALIGN bytes,
+    layer1.c:90, layer5.c:81) must be zero, as ParamSet.validate requires: the C ABI rejects a blob
+    whose pads are not (NET_ERR_BLOB), and accepts the unpatched blob."""
+    L = lib.load()
+    ps = ParamSet.synthetic(seed=3)
+    blob = bytearray(ps.to_blob())
+    assert L.net_params_load(bytes(blob), len(blob)) == lib.NET_OK
+    # layer-1 weights follow the 64-byte header and the two int32[F2] arrays; row f has C_ALIGN bytes
+    C, CA, F2 = ps.dims.C, ps.dims.C_ALIGN, 16
+    assert CA > C
+    b1 = bytearray(blob)
+    b1[64 + 2 * 4 * F2 + 3 * CA + C] = 1  # filter 3, first pad channel
+    assert L.net_params_load(bytes(b1), len(b1)) == lib.NET_ERR_BLOB
+    # layer-5 weights end the blob: [N][F2][T64_ALIGN]; the last byte is a pad column (T64 = 17 < 20)
+    assert ps.dims.T64 < ps.dims.T64_ALIGN
+    b5 = bytearray(blob)
+    b5[-1] = 0xFF
+    assert L.net_params_load(bytes(b5), len(b5)) == lib.NET_ERR_BLOB
+    lib.params_unload()
