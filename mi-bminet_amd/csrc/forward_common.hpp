@@ -128,6 +128,24 @@ struct L1Tile {
   float rr, cc;
 };
 
+// Two requant fmas / multiplies on float bit patterns, issued as two v_fma_f32 / v_mul_f32: packed
+// f32 VALU beside MFMAs costs more issue time than the two plain instructions (same-box A/B of
+// the fused kernel: -0.5 %, 13 of 15 interleaved rounds).  MIB_PACKED_FMA restores v_pk_fma_f32.
+__device__ __forceinline__ f2 fma2(int a, int b, float r, float c) {
+#ifndef MIB_PACKED_FMA
+  return (f2){__builtin_fmaf(__int_as_float(a), r, c), __builtin_fmaf(__int_as_float(b), r, c)};
+#else
+  return __builtin_elementwise_fma((f2){__int_as_float(a), __int_as_float(b)}, (f2){r, r}, (f2){c, c});
+#endif
+}
+__device__ __forceinline__ f2 mul2(float a, float b, float r) {
+#ifndef MIB_PACKED_FMA
+  return (f2){a * r, b * r};
+#else
+  return (f2){a, b} * (f2){r, r};
+#endif
+}
+
 // sum_{i<8} max(acc[base + i], thr) + off  (the REORDER_BN ReLU + sum-pool of layers 2 and 4)
 template <int BASE>
 __device__ __forceinline__ int pool8(const v16i& acc, int thr, int off) {

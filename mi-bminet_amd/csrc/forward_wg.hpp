@@ -421,9 +421,8 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
     }
 #endif
     // acc bits = 1.5*2^23 + (dot + off) as f32; fma(x, r, -1.5*2^23*r) == RN((dot+off)*r)
-    const f2 rr2 = {T.rr, T.rr}, cc2 = {T.cc, T.cc};
-    const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(acc[0]), __int_as_float(acc[1])}, rr2, cc2);
-    const f2 q23 = __builtin_elementwise_fma((f2){__int_as_float(acc[2]), __int_as_float(acc[3])}, rr2, cc2);
+    const f2 q01 = fma2(acc[0], acc[1], T.rr, T.cc);
+    const f2 q23 = fma2(acc[2], acc[3], T.rr, T.cc);
     int y[4] = {(int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]};  // trunc toward zero
     // lane column j = (filter 8t + j/2, parity j&1) when P == 2, filter j when P == 1;
     // row 4g + r = time group 16 blk + 4g + r
@@ -487,7 +486,7 @@ __device__ __forceinline__ unsigned l2n_out(const v16i& acc, float r, float c) {
 // Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].
 template <int LO>
 __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, float r) {
-  const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r, r};
+  const f2 q = mul2((float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off), r);
   return sat8x2<LO>((int)q[0], (int)q[1]);
 }
 
@@ -612,8 +611,8 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
     // C-init = float magic: acc bits = 1.5 * 2^23 + dot as f32, fma(bits, r, c) == RN(dot * r)
     v4i acc = {FMAGIC_I, FMAGIC_I, FMAGIC_I, FMAGIC_I};
     acc = __builtin_amdgcn_mfma_i32_16x16x32_i8(R.a3[fi], bv, acc, 0, 0, 0);
-    const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(acc[0]), __int_as_float(acc[1])}, (f2){r3, r3}, (f2){c3, c3});
-    const f2 q23 = __builtin_elementwise_fma((f2){__int_as_float(acc[2]), __int_as_float(acc[3])}, (f2){r3, r3}, (f2){c3, c3});
+    const f2 q01 = fma2(acc[0], acc[1], r3, c3);
+    const f2 q23 = fma2(acc[2], acc[3], r3, c3);
     w[fi] = sat8x4<K::LO>((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
   }
   // interleave the two filters: pair i = bytes (f0[i], f1[i])
@@ -642,7 +641,7 @@ __device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* s
   if constexpr (K::RB) {
     const int thr = MIB_K4(sp->l4_thr, int), off = MIB_K4(sp->l4_off, int);
     const float r4 = MIB_K4(sp->l4_r, float);
-    const f2 q = (f2){(float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off)} * (f2){r4, r4};
+    const f2 q = mul2((float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off), r4);
     return sat8x2<K::LO>((int)q[0], (int)q[1]);
   } else {
     // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
