@@ -21,6 +21,14 @@ constexpr int L2_TAPS = 64;
 constexpr int L3_TAPS = 16;
 constexpr int ND5_MAX = 96;     // dwords of the layer-4 output [F2][T64_ALIGN] (F2*T64_ALIGN <= 384)
 constexpr int FMAGIC_I = 0x4B400000;   // bit pattern of 1.5 * 2^23
+// REORDER_BN layer-2 pooling bias: the layer-2 MFMA chains start from a bias B (the bits of a
+// float MFMA srcC inline constant), so every conv value a lies at a + B with no wrap (|a| < 2^22),
+// and max(a, thr) - thr = sat_u32((a + B) - (thr + B)): one full-rate v_sub_u32 clamp per element
+// instead of a quarter-rate v_max_i32 (tools/vthru.hip: 2.45 vs 4.21 SIMD cycles).  Each chain
+// gets a constant of its own (filter slot 0: 1.0, slot 1: 2.0, the tail: 4.0): a constant shared
+// by two chains is hoisted into a 16-register tuple instead of riding in the instruction.
+__host__ __device__ constexpr int pbias(int slot) { return slot == 0 ? 0x3F800000 : slot == 1 ? 0x40000000 : 0x40800000; }
+constexpr int PBIAS_TAIL = 0x40800000;
 
 // Diagnostic phase stamps (tools/probe.hip builds with -DMIB_STAMPS; compiled out otherwise).
 #ifdef MIB_STAMPS
@@ -49,10 +57,10 @@ __host__ __device__ constexpr int odd_dwords(int x) { return ((x + 3) / 4 % 2) ?
 // Parameters read into LDS by every workgroup.
 struct SmallParams {
   v4i l4_bfrag[64];       // layer-4 B operand per lane (block diagonal, see host)
-  int l2_thr[F2];         // -(net_l2_offset >> 3)
-  int l2_off[F2];
+  int l2_thrt[F2];        // PBIAS_TAIL - (net_l2_offset >> 3): tail-chain pooling threshold
+  int l2_offm[F2];        // net_l2_offset + 8 thr = net_l2_offset & 7: offset after the relu form
   float l2_r[F2];
-  int l4_thr[F2];
+  int l4_thr[F2];         // -(net_l4_offset >> 3)
   int l4_off[F2];
   float l4_r[F2];
   // plain (non-REORDER_BN) layer-2/4 branches: per-element BN with offset >> 3 and factor >> 3,
@@ -78,8 +86,8 @@ struct DevParams {
   float l1_r[2][16];        // reciprocal per N-tile column
   float l1_c[2][16];        // -(1.5 * 2^23) * r, exact
   v4i l2_afrag[F2][3][64];  // layer-2 A operand (banded weights) per filter, K-step and lane
-  int l2_thr[F2];
-  int l2_off[F2];
+  int l2_thrb[F2];          // pbias(f & 1) - (net_l2_offset >> 3): full-tile pooling threshold
+  int l2_offm[F2];
   float l2_r[F2];
   long l3_afrag[F2][64];    // layer-3 A operand (16 shifts x 32-byte band) per filter and lane
   // layer-2 tail A operand per filter pair (wave) and K-step: MFMA 16x16x64, 16 shifts x 192
@@ -146,7 +154,22 @@ __device__ __forceinline__ f2 mul2(float a, float b, float r) {
 #endif
 }
 
-// sum_{i<8} max(acc[base + i], thr) + off  (the REORDER_BN ReLU + sum-pool of layers 2 and 4)
+// max(a, thr) - thr for a biased accumulator value acc = a + B and thrb = thr + B
+__device__ __forceinline__ unsigned relu_b(int acc, int thrb) {
+  return __builtin_elementwise_sub_sat((unsigned)acc, (unsigned)thrb);
+}
+
+// sum_{i<8} max(a[base + i], thr) + off = sum_{i<8} relu_b(acc[base + i], thrb) + offm, offm =
+// off + 8 thr  (the REORDER_BN ReLU + sum-pool of layer 2; acc = a + B)
+template <int BASE>
+__device__ __forceinline__ int pool8b(const v16i& acc, int thrb, int offm) {
+  unsigned m[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) m[i] = relu_b(acc[BASE + i], thrb);
+  return (int)(((m[0] + m[1] + m[2]) + (m[3] + m[4]) + (m[5] + m[6])) + (m[7] + (unsigned)offm));
+}
+
+// sum_{i<8} max(acc[base + i], thr) + off  (layer 4's REORDER_BN ReLU + sum-pool, unbiased)
 template <int BASE>
 __device__ __forceinline__ int pool8(const v16i& acc, int thr, int off) {
   int m[8];

@@ -267,9 +267,10 @@ struct Regs {
   __device__ __forceinline__ const L1Tile& tile(int t) const { return t == 0 ? t0 : t1; }
   __device__ __forceinline__ L1Tile& tile(int t) { return t == 0 ? t0 : t1; }
   v4i af[FPW][3];          // layer-2 band fragments of the wave's filters
-  int thr2[FPW], off2[FPW];  // REORDER_BN: threshold, offset; plain: MFMA C-init, magic c bits
+  int thr2[FPW], off2[FPW];  // REORDER_BN: biased threshold, offset + 8 thr; plain: MFMA C-init, magic c bits
   float r2[FPW];
   long a3[FPW];            // layer-3 band fragments of the wave's filters
+  float r3, c3;            // layer-3 requant constants (uniform)
   v4i pf[K::PF];           // layer-1 fragments prefetched one trial ahead
   int xoff;                // lane_xoff(lane)
 };
@@ -365,8 +366,8 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
 #pragma unroll
     for (int s = 0; s < 3; s++) R.af[fi][s] = prm->l2_afrag[f][s][lane];
     if constexpr (K::RB) {
-      R.thr2[fi] = prm->l2_thr[f];
-      R.off2[fi] = prm->l2_off[f];
+      R.thr2[fi] = prm->l2_thrb[f];
+      R.off2[fi] = prm->l2_offm[f];
       R.r2[fi] = prm->l2_r[f];
     } else {
       R.thr2[fi] = prm->sp.l2n_ci[f];
@@ -375,6 +376,8 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
     }
     R.a3[fi] = prm->l3_afrag[f][lane];
   }
+  R.r3 = prm->sp.l3_r;
+  R.c3 = prm->sp.l3_c;
   // small parameters -> LDS
   const v4i* src = (const v4i*)&prm->sp;
   v4i* dst = (v4i*)(smem + K::OFF_SP);
@@ -486,7 +489,7 @@ __device__ __forceinline__ unsigned l2n_out(const v16i& acc, float r, float c) {
 // Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].
 template <int LO>
 __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, float r) {
-  const f2 q = mul2((float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off), r);
+  const f2 q = mul2((float)pool8b<0>(acc, thr, off), (float)pool8b<8>(acc, thr, off), r);
   return sat8x2<LO>((int)q[0], (int)q[1]);
 }
 
@@ -505,12 +508,20 @@ __device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const Sma
   v4i bv[3], a[3];
 #pragma unroll
   for (int st = 0; st < 3; st++) {
-    const long* q = (const long*)(pb + T.tb[st]);  // 8-byte aligned
+#ifndef MIB_TAIL_READ2
+    // two ds_read_b64 (2 LDS cycles each) rather than the ds_read2_b64 the compiler would merge
+    // them into (8 cycles): the layer-2 interval is LDS-bound
+    typedef const volatile __attribute__((address_space(3))) long lds_vlong;
+    lds_vlong* q = (lds_vlong*)(pb + T.tb[st]);  // 8-byte aligned
+#else
+    const long* q = (const long*)(pb + T.tb[st]);
+#endif
     const long lo = q[0], hi = q[1];
     bv[st][0] = (int)lo; bv[st][1] = (int)(lo >> 32); bv[st][2] = (int)hi; bv[st][3] = (int)(hi >> 32);
     a[st] = tA[st * 64];
   }
-  v4i acc = {0, 0, 0, 0};
+  const int c0 = K::RB ? PBIAS_TAIL : 0;
+  v4i acc = {c0, c0, c0, c0};
 #pragma unroll
   for (int st = 0; st < 3; st++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[st], bv[st], acc, 0, 0, 0);
   // Operands stay live until the result is ready (see DESIGN.md on the tail chains).
@@ -525,8 +536,8 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
   const int fcol = wave * FPW + T.tp;
   int part;
   if constexpr (K::RB) {
-    const int thr = sp->l2_thr[fcol];
-    part = (max(tacc[0], thr) + max(tacc[1], thr)) + (max(tacc[2], thr) + max(tacc[3], thr));
+    const int thrb = sp->l2_thrt[fcol];
+    part = (int)((relu_b(tacc[0], thrb) + relu_b(tacc[1], thrb)) + (relu_b(tacc[2], thrb) + relu_b(tacc[3], thrb)));
   } else {
     const float r = sp->l2n_r[fcol], c = sp->l2n_c[fcol];
     const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(tacc[0]), __int_as_float(tacc[1])}, (f2){r, r}, (f2){c, c});
@@ -537,7 +548,7 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
   const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)part, (unsigned)part, false, false);
   const int tot = (int)sw[0] + (int)sw[1];  // whole window (rows 2k and 2k+1 hold the same)
   int y;
-  if constexpr (K::RB) y = rq<K::LO>(tot + sp->l2_off[fcol], sp->l2_r[fcol]);
+  if constexpr (K::RB) y = rq<K::LO>(tot + sp->l2_offm[fcol], sp->l2_r[fcol]);
   else y = tot >> 3;
   if (T.ty >= 0) smem_y2[wave * FPW * K::Y2ROW + T.ty] = (int8_t)y;
 }
@@ -556,7 +567,7 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
       const int8_t* pb = smem_y1 + f * K::Y1ROW + (32 / K::P) * 32 * mt + T.l2b - l2_boff<K>(0, 0);
       v16i acc;
 #pragma unroll
-      for (int i = 0; i < 16; i++) acc[i] = K::RB ? 0 : R.thr2[fi];  // plain branch: C-init
+      for (int i = 0; i < 16; i++) acc[i] = K::RB ? pbias(fi) : R.thr2[fi];  // plain branch: C-init
 #pragma unroll
       for (int s = 0; s < 3; s++)
 #ifdef MIB_DIAG_NOL2MFMA
@@ -591,6 +602,46 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
     const v4i tacc = layer2_tail_mfma<K>(smem_y1, sp, T, wave, lane);
     layer2_tail_out<K>(tacc, smem_y2, sp, T, wave);
   }
+  // Sensitivity diagnostics (tools/ab.py builds only): extra independent work per wave and trial
+#ifdef MIB_DIAG_XVALU
+#if MIB_DIAG_XSEL == 1
+#define MIB_DIAG_XOP "v_add_u32"
+#elif MIB_DIAG_XSEL == 2
+#define MIB_DIAG_XOP "v_cvt_f32_i32"
+#else
+#define MIB_DIAG_XOP "v_max_i32"
+#endif
+  {
+    int d0 = lane, d1 = lane + 1, d2 = lane + 2, d3 = lane + 3;
+    const int xs = R.xoff;
+#pragma unroll
+    for (int i = 0; i < MIB_DIAG_XVALU / 4; i++)
+      asm volatile(MIB_DIAG_XOP " %0, %0, %4\n" MIB_DIAG_XOP " %1, %1, %4\n" MIB_DIAG_XOP " %2, %2, %4\n" MIB_DIAG_XOP " %3, %3, %4"
+                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3) : "v"(xs));
+    asm volatile("" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3));
+  }
+#endif
+#ifdef MIB_DIAG_XMFMA
+  {
+    v4i d = {0, 0, 0, 0};
+    const v4i bb = *(const v4i*)(smem_y1 + wave * FPW * K::Y1ROW + T.l2b);
+#pragma unroll
+    for (int i = 0; i < MIB_DIAG_XMFMA; i++) asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(d) : "v"(R.af[0][i % 3]), "v"(bb));
+    asm volatile("s_nop 7\n s_nop 7" ::"v"(d));
+  }
+#endif
+#ifdef MIB_DIAG_XLDS
+  {
+    v4i s = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < MIB_DIAG_XLDS; i++) {
+      v4i t;
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(t) : "v"(T.l2b), "i"(16 * (i % 8)));
+      s ^= t;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(s));
+  }
+#endif
 }
 
 // ---- layer 3 ---------------------------------------------------------------------------------
@@ -602,7 +653,11 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 template <class K>
 __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, const SmallParams* sp,
                                        const Regs<K>& R, const LaneTab& T, int wave) {
+#ifndef MIB_L3C_LDS
+  const float r3 = R.r3, c3 = R.c3;  // wave-uniform (SGPRs): no LDS read per trial
+#else
   const float r3 = sp->l3_r, c3 = sp->l3_c;
+#endif
   unsigned w[FPW];
 #pragma unroll
   for (int fi = 0; fi < FPW; fi++) {

@@ -273,13 +273,15 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         }
         std::memcpy(&dp.l2_afrag[f][s][lane], bytes, 16);
       }
-    dp.l2_thr[f] = -(hp.l2_offset[f] >> 3);
-    dp.l2_off[f] = hp.l2_offset[f];
+    // pooling in the biased relu form (forward_common.hpp, pool8): thr = -(off >> 3) (layer2.c)
+    const int32_t thr2 = -(hp.l2_offset[f] >> 3);
+    dp.l2_thrb[f] = pbias(f & 1) + thr2;  // the wave's filter slot f & 1 (forward_wg.hpp, layer2)
+    dp.l2_offm[f] = hp.l2_offset[f] + 8 * thr2;
     // pooled sum + offset lies in [0, 8 * 64 * A + |off|] (8 * (off >> 3) <= off)
     const int64_t v2 = 8LL * 64 * A + std::llabs((int64_t)hp.l2_offset[f]);
     if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f], nullptr, 128, v2)) return NET_ERR_RANGE;
-    dp.sp.l2_thr[f] = dp.l2_thr[f];
-    dp.sp.l2_off[f] = dp.l2_off[f];
+    dp.sp.l2_thrt[f] = PBIAS_TAIL + thr2;
+    dp.sp.l2_offm[f] = dp.l2_offm[f];
     dp.sp.l2_r[f] = dp.l2_r[f];
 
   }

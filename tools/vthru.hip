@@ -109,6 +109,12 @@ DEFK(k_subrevu, OP_SUBREVU)
 DEFK(k_minf, OP_MINF)
 #define OP_MINI(x) asm volatile("v_min_i32 %0, %0, %1" : "+v"(x) : "v"(k));
 DEFK(k_mini, OP_MINI)
+#define OP_SUBUCL(x) asm volatile("v_sub_u32_e64 %0, %0, %1 clamp" : "+v"(x) : "v"(k));
+DEFK(k_subucl, OP_SUBUCL)
+#define OP_MAXI64(x) asm volatile("v_max_i32_e64 %0, %0, %1" : "+v"(x) : "v"(k));
+DEFK(k_maxi64, OP_MAXI64)
+#define OP_SUBICL(x) asm volatile("v_sub_i32 %0, %0, %1 clamp" : "+v"(x) : "v"(k));
+DEFK(k_subicl, OP_SUBICL)
 #define OP_DPP(x) asm volatile("v_add_u32_dpp %0, %1, %0 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(x) : "v"(k));
 DEFK(k_dpp, OP_DPP)
 
@@ -244,7 +250,7 @@ int main() {
   long long* dcyc;
   hipMalloc(&dout, 4096 * 4);
   hipMalloc(&dcyc, 64);
-  struct { const char* n; KF f; } ks[] = {{"v_max_i32", k_maxi}, {"v_add_u32", k_addu}, {"v_add_u32_e64", k_addu64}, {"v_sub_u32", k_subu}, {"v_add3_u32", k_add3}, {"v_cvt_i32_f32", k_cvti}, {"v_cvt_f32_i32", k_cvtf}, {"v_fma_f32", k_fma}, {"v_max_f32", k_maxf}, {"v_mul_f32", k_mulf}, {"v_add_f32", k_addf}, {"v_add_f32_e64", k_addfabs}, {"v_ashr_pk_i8_i32", k_ashrpk}, {"v_ashr_pk_u8_i32", k_ashrpku}, {"v_perm_b32", k_perm}, {"v_med3_i32", k_med3}, {"v_med3_f32", k_med3f}, {"v_pk_max_i16", k_pkmaxi16}, {"v_pk_add_u16", k_pkaddu16}, {"v_max3_i32", k_max3i}, {"v_lshl_or_b32", k_lshlor}, {"v_and_b32", k_andb}, {"v_or_b32", k_orb}, {"v_xor_b32", k_xorb}, {"v_lshlrev_b32", k_lshl}, {"v_ashrrev_i32", k_ashr}, {"v_cvt_pk_i16_i32", k_cvtpki16}, {"v_sat_pk_u8_i16", k_satpku8}, {"v_cvt_pk_u8_f32", k_cvtpku8}, {"v_cvt_pknorm_i16_f32", k_cvtpknorm}, {"v_dot4_i32_i8", k_sdot4}, {"v_mad_i32_i24", k_mad24}, {"v_max_u32", k_maxu}, {"v_mov_b32", k_movb}, {"v_cndmask_b32", k_cndm}, {"v_bfe_i32", k_bfe}, {"v_add_i32", k_addi32}, {"v_maximum3_f32", k_maximum3f}, {"v_bitop3_b32", k_bitop3}, {"v_subrev_u32", k_subrevu}, {"v_min_f32", k_minf}, {"v_min_i32", k_mini}, {"v_add_u32_dpp", k_dpp}, {"v_cndmask(vcc set)", k_cnd_vcc}, {"v_cndmask_e64(sgpr)", k_cnd_sgpr}, {"v_cvt_i32_f32_sdwa(byte1,preserve)", k_cvtsdwa}, {"v_cvt_i32_f32_sdwa(byte0,pad)", k_cvtsdwa0}, {"v_pk_fma_f32 clamp", k_pkfmac}, {"v_pk_fma_f32", k_pkfma}, {"v_pk_add_f32", k_pkadd}};
+  struct { const char* n; KF f; } ks[] = {{"v_max_i32", k_maxi}, {"v_add_u32", k_addu}, {"v_add_u32_e64", k_addu64}, {"v_sub_u32", k_subu}, {"v_add3_u32", k_add3}, {"v_cvt_i32_f32", k_cvti}, {"v_cvt_f32_i32", k_cvtf}, {"v_fma_f32", k_fma}, {"v_max_f32", k_maxf}, {"v_mul_f32", k_mulf}, {"v_add_f32", k_addf}, {"v_add_f32_e64", k_addfabs}, {"v_ashr_pk_i8_i32", k_ashrpk}, {"v_ashr_pk_u8_i32", k_ashrpku}, {"v_perm_b32", k_perm}, {"v_med3_i32", k_med3}, {"v_med3_f32", k_med3f}, {"v_pk_max_i16", k_pkmaxi16}, {"v_pk_add_u16", k_pkaddu16}, {"v_max3_i32", k_max3i}, {"v_lshl_or_b32", k_lshlor}, {"v_and_b32", k_andb}, {"v_or_b32", k_orb}, {"v_xor_b32", k_xorb}, {"v_lshlrev_b32", k_lshl}, {"v_ashrrev_i32", k_ashr}, {"v_cvt_pk_i16_i32", k_cvtpki16}, {"v_sat_pk_u8_i16", k_satpku8}, {"v_cvt_pk_u8_f32", k_cvtpku8}, {"v_cvt_pknorm_i16_f32", k_cvtpknorm}, {"v_dot4_i32_i8", k_sdot4}, {"v_mad_i32_i24", k_mad24}, {"v_max_u32", k_maxu}, {"v_mov_b32", k_movb}, {"v_cndmask_b32", k_cndm}, {"v_bfe_i32", k_bfe}, {"v_add_i32", k_addi32}, {"v_maximum3_f32", k_maximum3f}, {"v_bitop3_b32", k_bitop3}, {"v_subrev_u32", k_subrevu}, {"v_min_f32", k_minf}, {"v_min_i32", k_mini}, {"v_add_u32_dpp", k_dpp}, {"v_sub_u32_e64 clamp", k_subucl}, {"v_max_i32_e64", k_maxi64}, {"v_sub_i32 clamp", k_subicl}, {"v_cndmask(vcc set)", k_cnd_vcc}, {"v_cndmask_e64(sgpr)", k_cnd_sgpr}, {"v_cvt_i32_f32_sdwa(byte1,preserve)", k_cvtsdwa}, {"v_cvt_i32_f32_sdwa(byte0,pad)", k_cvtsdwa0}, {"v_pk_fma_f32 clamp", k_pkfmac}, {"v_pk_fma_f32", k_pkfma}, {"v_pk_add_f32", k_pkadd}};
   const double n = 64.0 * 8 * 8;
   printf("SIMD cycles per wave-instruction (1 / 2 / 4 waves per SIMD)\n");
   for (auto& k : ks) {
