@@ -61,7 +61,7 @@ struct SmallParams {
   int l2_offm[F2];        // net_l2_offset + 8 thr = net_l2_offset & 7: offset after the relu form
   float l2_r[F2];
   int l4_thr[F2];         // -(net_l4_offset >> 3)
-  int l4_off[F2];
+  int l4_offm[F2];        // net_l4_offset + 8 thr
   float l4_r[F2];
   // plain (non-REORDER_BN) layer-2/4 branches: per-element BN with offset >> 3 and factor >> 3,
   // as magic-offset MFMA C-init (offset + FMAGIC_I), reciprocal and -(1.5 * 2^23) * r
@@ -160,7 +160,7 @@ __device__ __forceinline__ unsigned relu_b(int acc, int thrb) {
 }
 
 // sum_{i<8} max(a[base + i], thr) + off = sum_{i<8} relu_b(acc[base + i], thrb) + offm, offm =
-// off + 8 thr  (the REORDER_BN ReLU + sum-pool of layer 2; acc = a + B)
+// off + 8 thr  (the REORDER_BN ReLU + sum-pool of layers 2 and 4; acc = a + B)
 template <int BASE>
 __device__ __forceinline__ int pool8b(const v16i& acc, int thrb, int offm) {
   unsigned m[8];
@@ -169,13 +169,6 @@ __device__ __forceinline__ int pool8b(const v16i& acc, int thrb, int offm) {
   return (int)(((m[0] + m[1] + m[2]) + (m[3] + m[4]) + (m[5] + m[6])) + (m[7] + (unsigned)offm));
 }
 
-// sum_{i<8} max(acc[base + i], thr) + off  (layer 4's REORDER_BN ReLU + sum-pool, unbiased)
-template <int BASE>
-__device__ __forceinline__ int pool8(const v16i& acc, int thr, int off) {
-  int m[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) m[i] = max(acc[BASE + i], thr);
-  return ((m[0] + m[1] + m[2]) + (m[3] + m[4]) + (m[5] + m[6])) + (m[7] + off);
-}
+
 
 }  // namespace mib

@@ -689,14 +689,18 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
 // K-slots 16h..16h+15; B is block diagonal (columns c < 16: channel c on slots 0..15, columns
 // c >= 16: channel c-16 on slots 16..31), so column c of D = channel c & 15 of time block c >> 4.
 // Rows n(i) permuted so lane (c, h) register r = time 16h + r of that block: two pool-8 windows.
+// REORDER_BN: part t's MFMA starts from bias4(t) (biased relu pooling as in layer 2, a constant of
+// its own per part so that none is hoisted into registers)
+__host__ __device__ constexpr int bias4(int t) { return t == 0 ? (int)0x3F000000 : t == 1 ? (int)0xBF000000 : (int)0xBF800000; }
+
 template <class K>
-__device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* sp, int kb) {
+__device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* sp, int kb, int bias) {
   // kb = 4 k (byte offset of channel k)
 #define MIB_K4(arr, T) (*(const T*)((const char*)(arr) + kb))
   if constexpr (K::RB) {
-    const int thr = MIB_K4(sp->l4_thr, int), off = MIB_K4(sp->l4_off, int);
+    const int thrb = MIB_K4(sp->l4_thr, int) + bias, offm = MIB_K4(sp->l4_offm, int);
     const float r4 = MIB_K4(sp->l4_r, float);
-    const f2 q = mul2((float)pool8<0>(acc, thr, off), (float)pool8<8>(acc, thr, off), r4);
+    const f2 q = mul2((float)pool8b<0>(acc, thrb, offm), (float)pool8b<8>(acc, thrb, offm), r4);
     return sat8x2<K::LO>((int)q[0], (int)q[1]);
   } else {
     // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
@@ -735,16 +739,16 @@ __device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, c
     for (int t = 0; t < K::NT4; t++) a[t] = *(const v4i*)(smem_y3 + L.l4a + y3_off<K>(64 * t));  // unaligned (4 B)
     v16i acc[2];
 #pragma unroll
-    for (int j = 0; j < 16; j++) acc[0][j] = ci;
+    for (int j = 0; j < 16; j++) acc[0][j] = K::RB ? bias4(0) : ci;
     acc[0] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], bw, acc[0], 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < K::NT4; t++) {
       if (t + 1 < K::NT4) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) acc[(t + 1) & 1][j] = ci;
+        for (int j = 0; j < 16; j++) acc[(t + 1) & 1][j] = K::RB ? bias4(t + 1) : ci;
         acc[(t + 1) & 1] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[t + 1 < K::NT4 ? t + 1 : 0], bw, acc[(t + 1) & 1], 0, 0, 0);
       }
-      const unsigned w = l4_out<K>(acc[t & 1], sp, L.l4k);
+      const unsigned w = l4_out<K>(acc[t & 1], sp, L.l4k, bias4(t));
       if ((L.l4m >> t) & 1) *(unsigned short*)(smem_y4 + L.l4w + 8 * t) = (unsigned short)w;
     }
   } else {
@@ -753,9 +757,9 @@ __device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, c
       const v4i a = *(const v4i*)(smem_y3 + L.l4a + y3_off<K>(64 * t));  // unaligned (4 B)
       v16i acc;
 #pragma unroll
-      for (int j = 0; j < 16; j++) acc[j] = ci;
+      for (int j = 0; j < 16; j++) acc[j] = K::RB ? bias4(t) : ci;
       acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bw, acc, 0, 0, 0);
-      const unsigned w = l4_out<K>(acc, sp, L.l4k);
+      const unsigned w = l4_out<K>(acc, sp, L.l4k, bias4(t));
       if ((L.l4m >> t) & 1) *(unsigned short*)(smem_y4 + L.l4w + 8 * t) = (unsigned short)w;
     }
   }

@@ -334,7 +334,7 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
   }
   for (int k = 0; k < F2; k++) {
     sp.l4_thr[k] = -(hp.l4_offset[k] >> 3);
-    sp.l4_off[k] = hp.l4_offset[k];
+    sp.l4_offm[k] = hp.l4_offset[k] + 8 * sp.l4_thr[k];  // biased relu pooling (forward_wg.hpp, l4_out)
     const int64_t v4 = 8LL * F2 * A + std::llabs((int64_t)hp.l4_offset[k]);
     if (!choose_reciprocal(hp.l4_factor[k], &sp.l4_r[k], nullptr, 128, v4)) return NET_ERR_RANGE;
   }
