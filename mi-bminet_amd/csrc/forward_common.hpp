@@ -57,9 +57,8 @@ __host__ __device__ constexpr int odd_dwords(int x) { return ((x + 3) / 4 % 2) ?
 // Parameters read into LDS by every workgroup.
 struct SmallParams {
   v4i l4_bfrag[64];       // layer-4 B operand per lane (block diagonal, see host)
-  int l2_thrt[F2];        // PBIAS_TAIL - (net_l2_offset >> 3): tail-chain pooling threshold
-  int l2_offm[F2];        // net_l2_offset + 8 thr = net_l2_offset & 7: offset after the relu form
-  float l2_r[F2];
+  v4i l2_tpar[F2];        // layer-2 tail per filter: {PBIAS_TAIL + thr, off + 8 thr, bits of r, 0}
+                          // (thr = -(net_l2_offset >> 3); off + 8 thr = net_l2_offset & 7)
   int l4_thr[F2];         // -(net_l4_offset >> 3)
   int l4_offm[F2];        // net_l4_offset + 8 thr
   float l4_r[F2];
@@ -139,12 +138,13 @@ struct L1Tile {
 // Two requant fmas / multiplies on float bit patterns, issued as two v_fma_f32 / v_mul_f32: packed
 // f32 VALU beside MFMAs costs more issue time than the two plain instructions (same-box A/B of
 // the fused kernel: -0.5 %, 13 of 15 interleaved rounds).  MIB_PACKED_FMA restores v_pk_fma_f32.
+template <bool PACKED = false>
 __device__ __forceinline__ f2 fma2(int a, int b, float r, float c) {
 #ifndef MIB_PACKED_FMA
-  return (f2){__builtin_fmaf(__int_as_float(a), r, c), __builtin_fmaf(__int_as_float(b), r, c)};
-#else
-  return __builtin_elementwise_fma((f2){__int_as_float(a), __int_as_float(b)}, (f2){r, r}, (f2){c, c});
+  if constexpr (!PACKED)
+    return (f2){__builtin_fmaf(__int_as_float(a), r, c), __builtin_fmaf(__int_as_float(b), r, c)};
 #endif
+  return __builtin_elementwise_fma((f2){__int_as_float(a), __int_as_float(b)}, (f2){r, r}, (f2){c, c});
 }
 __device__ __forceinline__ f2 mul2(float a, float b, float r) {
 #ifndef MIB_PACKED_FMA

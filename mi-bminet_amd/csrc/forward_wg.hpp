@@ -508,14 +508,7 @@ __device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const Sma
   v4i bv[3], a[3];
 #pragma unroll
   for (int st = 0; st < 3; st++) {
-#ifndef MIB_TAIL_READ2
-    // two ds_read_b64 (2 LDS cycles each) rather than the ds_read2_b64 the compiler would merge
-    // them into (8 cycles): the layer-2 interval is LDS-bound
-    typedef const volatile __attribute__((address_space(3))) long lds_vlong;
-    lds_vlong* q = (lds_vlong*)(pb + T.tb[st]);  // 8-byte aligned
-#else
-    const long* q = (const long*)(pb + T.tb[st]);
-#endif
+    const long* q = (const long*)(pb + T.tb[st]);  // 8-byte aligned
     const long lo = q[0], hi = q[1];
     bv[st][0] = (int)lo; bv[st][1] = (int)(lo >> 32); bv[st][2] = (int)hi; bv[st][3] = (int)(hi >> 32);
     a[st] = tA[st * 64];
@@ -534,9 +527,10 @@ template <class K>
 __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2, const SmallParams* sp,
                                                 const LaneTab& T, int wave) {
   const int fcol = wave * FPW + T.tp;
+  const v4i tp = K::RB ? sp->l2_tpar[fcol] : (v4i){0, 0, 0, 0};  // {thr + PBIAS_TAIL, offm, r}
   int part;
   if constexpr (K::RB) {
-    const int thrb = sp->l2_thrt[fcol];
+    const int thrb = tp[0];
     part = (int)((relu_b(tacc[0], thrb) + relu_b(tacc[1], thrb)) + (relu_b(tacc[2], thrb) + relu_b(tacc[3], thrb)));
   } else {
     const float r = sp->l2n_r[fcol], c = sp->l2n_c[fcol];
@@ -548,7 +542,7 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
   const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)part, (unsigned)part, false, false);
   const int tot = (int)sw[0] + (int)sw[1];  // whole window (rows 2k and 2k+1 hold the same)
   int y;
-  if constexpr (K::RB) y = rq<K::LO>(tot + sp->l2_offm[fcol], sp->l2_r[fcol]);
+  if constexpr (K::RB) y = rq<K::LO>(tot + tp[1], __int_as_float(tp[2]));
   else y = tot >> 3;
   if (T.ty >= 0) smem_y2[wave * FPW * K::Y2ROW + T.ty] = (int8_t)y;
 }
@@ -666,8 +660,10 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
     // C-init = float magic: acc bits = 1.5 * 2^23 + dot as f32, fma(bits, r, c) == RN(dot * r)
     v4i acc = {FMAGIC_I, FMAGIC_I, FMAGIC_I, FMAGIC_I};
     acc = __builtin_amdgcn_mfma_i32_16x16x32_i8(R.a3[fi], bv, acc, 0, 0, 0);
-    const f2 q01 = fma2(acc[0], acc[1], r3, c3);
-    const f2 q23 = fma2(acc[2], acc[3], r3, c3);
+    // packed here (same-box A/B -0.8 %), plain v_fma_f32 in layer 1 (packed +0.2 %, beside MFMAs)
+    constexpr bool PK3 = true;
+    const f2 q01 = fma2<PK3>(acc[0], acc[1], r3, c3);
+    const f2 q23 = fma2<PK3>(acc[2], acc[3], r3, c3);
     w[fi] = sat8x4<K::LO>((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
   }
   // interleave the two filters: pair i = bytes (f0[i], f1[i])

@@ -280,9 +280,9 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     // pooled sum + offset lies in [0, 8 * 64 * A + |off|] (8 * (off >> 3) <= off)
     const int64_t v2 = 8LL * 64 * A + std::llabs((int64_t)hp.l2_offset[f]);
     if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f], nullptr, 128, v2)) return NET_ERR_RANGE;
-    dp.sp.l2_thrt[f] = PBIAS_TAIL + thr2;
-    dp.sp.l2_offm[f] = dp.l2_offm[f];
-    dp.sp.l2_r[f] = dp.l2_r[f];
+    int32_t rbits;
+    std::memcpy(&rbits, &dp.l2_r[f], 4);
+    dp.sp.l2_tpar[f] = (v4i){PBIAS_TAIL + thr2, dp.l2_offm[f], rbits, 0};
 
   }
   // layer-2 tail bands (forward_wg.hpp, layer2_tail_mfma): filter pair w = filters 2w, 2w+1;
