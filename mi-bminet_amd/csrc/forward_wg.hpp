@@ -647,11 +647,7 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 template <class K>
 __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, const SmallParams* sp,
                                        const Regs<K>& R, const LaneTab& T, int wave) {
-#ifndef MIB_L3C_LDS
   const float r3 = R.r3, c3 = R.c3;  // wave-uniform (SGPRs): no LDS read per trial
-#else
-  const float r3 = sp->l3_r, c3 = sp->l3_c;
-#endif
   unsigned w[FPW];
 #pragma unroll
   for (int fi = 0; fi < FPW; fi++) {
