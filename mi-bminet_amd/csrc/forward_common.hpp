@@ -21,14 +21,15 @@ constexpr int L2_TAPS = 64;
 constexpr int L3_TAPS = 16;
 constexpr int ND5_MAX = 96;     // dwords of the layer-4 output [F2][T64_ALIGN] (F2*T64_ALIGN <= 384)
 constexpr int FMAGIC_I = 0x4B400000;   // bit pattern of 1.5 * 2^23
-// REORDER_BN layer-2 pooling bias: the layer-2 MFMA chains start from a bias B (the bits of a
+// REORDER_BN pooling bias: the layer-2 MFMA chains start from a bias B (the bits of a
 // float MFMA srcC inline constant), so every conv value a lies at a + B with no wrap (|a| < 2^22),
 // and max(a, thr) - thr = sat_u32((a + B) - (thr + B)): one full-rate v_sub_u32 clamp per element
 // instead of a quarter-rate v_max_i32 (tools/vthru.hip: 2.45 vs 4.21 SIMD cycles).  Each chain
 // gets a constant of its own (filter slot 0: 1.0, slot 1: 2.0, the tail: 4.0): a constant shared
 // by two chains is hoisted into a 16-register tuple instead of riding in the instruction.
+// (layer 4 uses 0.5, -0.5 and -1.0: forward_wg.hpp, bias4)
 __host__ __device__ constexpr int pbias(int slot) { return slot == 0 ? 0x3F800000 : slot == 1 ? 0x40000000 : 0x40800000; }
-constexpr int PBIAS_TAIL = 0x40800000;
+constexpr int PBIAS_TAIL = pbias(2);
 
 // Diagnostic phase stamps (tools/probe.hip builds with -DMIB_STAMPS; compiled out otherwise).
 #ifdef MIB_STAMPS
@@ -85,8 +86,8 @@ struct DevParams {
   float l1_r[2][16];        // reciprocal per N-tile column
   float l1_c[2][16];        // -(1.5 * 2^23) * r, exact
   v4i l2_afrag[F2][3][64];  // layer-2 A operand (banded weights) per filter, K-step and lane
-  int l2_thrb[F2];          // pbias(f & 1) - (net_l2_offset >> 3): full-tile pooling threshold
-  int l2_offm[F2];
+  int l2_thrb[F2];          // pbias(f & 1) + thr, thr = -(net_l2_offset >> 3): full-tile threshold
+  int l2_offm[F2];          // net_l2_offset + 8 thr
   float l2_r[F2];
   long l3_afrag[F2][64];    // layer-3 A operand (16 shifts x 32-byte band) per filter and lane
   // layer-2 tail A operand per filter pair (wave) and K-step: MFMA 16x16x64, 16 shifts x 192
@@ -168,7 +169,5 @@ __device__ __forceinline__ int pool8b(const v16i& acc, int thrb, int offm) {
   for (int i = 0; i < 8; i++) m[i] = relu_b(acc[BASE + i], thrb);
   return (int)(((m[0] + m[1] + m[2]) + (m[3] + m[4]) + (m[5] + m[6])) + (m[7] + (unsigned)offm));
 }
-
-
 
 }  // namespace mib
