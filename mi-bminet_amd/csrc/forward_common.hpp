@@ -89,7 +89,11 @@ struct DevParams {
   int l2_thrb[F2];          // pbias(f & 1) + thr, thr = -(net_l2_offset >> 3): full-tile threshold
   int l2_offm[F2];          // net_l2_offset + 8 thr
   float l2_r[F2];
-  long l3_afrag[F2][64];    // layer-3 A operand (16 shifts x 32-byte band) per filter and lane
+  // layer-3 A operands per filter pair (wave) and lane, MFMA 16x16x64 with a block-diagonal K
+  // (forward_wg.hpp, layer3): tile 1 = 16 shifts x both filters' 32-slot bands, tile 2 = the same
+  // with shift g on row 4g and the other rows zero
+  v4i l3_a1[F2 / 2][64];
+  v4i l3_a2[F2 / 2][64];
   // layer-2 tail A operand per filter pair (wave) and K-step: MFMA 16x16x64, 16 shifts x 192
   // K-slots = the two filters' 96-slot bands side by side (K block diagonal, see forward_wg.hpp)
   v4i l2t_afrag[F2 / 2][3][64];
@@ -126,6 +130,18 @@ __device__ __forceinline__ unsigned sat8x4(int a, int b, int c, int d) {
   unsigned r = sat8x2<LO>(a, b);
   asm("v_ashr_pk_i8_i32 %0, %1, %2, 0 op_sel:[0,0,0,1]" : "+v"(r) : "v"(c), "v"(d));
   return r;
+}
+
+// sat8x4 through the compiler builtin (no inline asm): the compiler sees the instructions and
+// orders them against MFMAs still in flight (layer 3, whose tile 2 uses only part of its result);
+// the high pair costs a shift and an OR instead of op_sel
+template <int LO = -128>
+__device__ __forceinline__ unsigned sat8x4_b(int a, int b, int c, int d) {
+  if constexpr (LO != -128) {
+    a = max(a, LO); b = max(b, LO); c = max(c, LO); d = max(d, LO);
+  }
+  const unsigned lo = __builtin_amdgcn_ashr_pk_i8_i32(a, b, 0), hi = __builtin_amdgcn_ashr_pk_i8_i32(c, d, 0);
+  return (lo & 0xFFFFu) | (hi << 16);
 }
 
 // Layer-1 per-lane constants of one N-tile (kept as a scalarisable struct: arrays of these

@@ -112,7 +112,14 @@ struct Cfg {
   static constexpr int Y1ROW = P * PLANE;
   static constexpr int XTRIAL = align16(T * C);         // batched trial stride (bytes)
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
-  static constexpr int Y2ROW = odd_dwords(cmax(T8 + 24, 16 * NB3 + 24));
+  // layer 3: tile 1 = the first L3C blocks of both filters side by side (one 16x16x64 MFMA),
+  // tile 2 = the L3R outputs past 128, four per column in register 0 only (layer3)
+  static constexpr int L3C = cmin(NB3, 8);
+  static constexpr int L3R = T8 > 128 ? T8 - 128 : 0;
+  static constexpr int L3RC = (L3R + 3) / 4;
+  // y2 row: pad [0, 8), positions at 8 + u, zero pads after; the last 16 bytes are the zero chunk
+  // that block-diagonal B operands read (tile 1 reads bytes < 16 L3C + 16, tile 2 < 128 + 4 L3RC + 28)
+  static constexpr int Y2ROW = align16(cmax(cmax(T8 + 8, 16 * L3C + 16), L3RC ? 128 + 4 * L3RC + 28 : 0) + 16);
   static constexpr int Y3ROWS = cmax(64 * NT4, T8);
   // y3t row u (16 filters) starts at byte 16 u + 4 (u >> 4) (y3_off): layer 3's 2-byte stores
   // (one wave instruction covers rows 16 col + 4 g + i of 32 lanes) then hit 32 different banks;
@@ -138,6 +145,8 @@ struct Cfg {
   static_assert(16 * N5L <= ND5_MAX, "layer-5 input too long");
   static_assert(MT >= 1, "at least one full layer-2 tile");
   static_assert(FPW * TC <= 16, "tail columns of a wave fit one 16-column tile");
+  static_assert(L3RC <= 8, "layer-3 tile 2 covers at most 32 outputs past 128");
+  static_assert(Y3ROWS >= 16 * L3C, "layer-3 tile-1 rows fit y3t");
 };
 
 // byte offset of layer-1 output (filter f, sample t) inside the LDS rows
@@ -157,9 +166,13 @@ struct LaneTab {
              // the K-step's slots of this lane belong to the other filter)
   int ty;   // tail y2 store: fi_c * Y2ROW + 8 + u, or -1 (lane stores nothing)
   int tp;   // tail: filter slot fi_c of this lane's column (0 or 1)
-  int l3b;  // layer-3 B slice: 16 col + 8 g
-  int l3w;  // layer-3 store: y3_off(16 col + 4 g), or -1 (rows past T8)
-  int pad[3];
+  int l3b;  // layer-3 tile-1 B chunk (16-byte aligned, relative to the wave's y2 rows): filter
+            // fi = col >> 3, block col & 7: fi Y2ROW + 16 (col & 7) + 16 (g & 1) when lane group g
+            // lies in the filter's K half (g >> 1 == fi), else the zero chunk
+  int l3w;  // tile-1 store: y3_off(r0), r0 = 16 (col & 7) + 4 g + 2 fi (rows r0, r0 + 1), or -1
+  int l3s;  // tile-1 v_perm selector pairing the lane's bytes with its partner's (col ^ 8)
+  int l3b2; // tile-2 B chunk (4-byte aligned): fi Y2ROW + 128 + 4 (col & 7) + 16 (g & 1), or zero chunk
+  int l3w2; // tile-2 store: y3_off(128 + 4 (col & 7) + g) + fi, or -1
 };
 static_assert(sizeof(LaneTab) == 48, "LaneTab is read as three 16-byte pieces");
 
@@ -252,11 +265,17 @@ __device__ __forceinline__ LaneTab build_lane_tab(int lane) {
     const int u = 128 * K::MT + 2 * bq + (g >> 1);
     T.ty = (cvalid && !(g & 1) && u < K::T8) ? fs * K::Y2ROW + 8 + u : -1;
     T.tp = fs;
-    T.l3b = 16 * col + 8 * g;
-    const int u3 = 16 * col + 4 * g;
-    T.l3w = u3 < K::T8 ? y3_off<K>(u3) : -1;
+    // layer 3 (see layer3): lane (col, g), filter slot fi = col >> 3, column j = col & 7
+    const int fi3 = col >> 3, j3 = col & 7;
+    const int zero = K::Y2ROW - 16;
+    T.l3b = ((g >> 1) == fi3 && j3 < K::L3C) ? fi3 * K::Y2ROW + 16 * j3 + 16 * (g & 1) : zero;
+    const int u3 = 16 * j3 + 4 * g;
+    T.l3w = (j3 < K::L3C && u3 < K::T8) ? y3_off<K>(u3 + 2 * fi3) : -1;
+    T.l3s = fi3 == 0 ? 0x05010400 : 0x03070206;
+    T.l3b2 = ((g >> 1) == fi3 && j3 < K::L3RC) ? fi3 * K::Y2ROW + 128 + 4 * j3 + 16 * (g & 1) : zero;
+    const int v3 = 128 + 4 * j3 + g;
+    T.l3w2 = (j3 < K::L3RC && v3 < K::T8) ? y3_off<K>(v3) + fi3 : -1;
   }
-  T.pad[0] = T.pad[1] = T.pad[2] = 0;
   return T;
 }
 
@@ -269,7 +288,7 @@ struct Regs {
   v4i af[FPW][3];          // layer-2 band fragments of the wave's filters
   int thr2[FPW], off2[FPW];  // REORDER_BN: biased threshold, offset + 8 thr; plain: MFMA C-init, magic c bits
   float r2[FPW];
-  long a3[FPW];            // layer-3 band fragments of the wave's filters
+  v4i a31, a32;            // layer-3 tile-1 / tile-2 band fragments of the wave's filter pair
   float r3, c3;            // layer-3 requant constants (uniform)
   v4i pf[K::PF];           // layer-1 fragments prefetched one trial ahead
   int xoff;                // lane_xoff(lane)
@@ -374,8 +393,9 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
       R.off2[fi] = __float_as_int(prm->sp.l2n_c[f]);
       R.r2[fi] = prm->sp.l2n_r[f];
     }
-    R.a3[fi] = prm->l3_afrag[f][lane];
   }
+  R.a31 = prm->l3_a1[wave][lane];
+  R.a32 = prm->l3_a2[wave][lane];
   R.r3 = prm->sp.l3_r;
   R.c3 = prm->sp.l3_c;
   // small parameters -> LDS
@@ -639,40 +659,46 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 }
 
 // ---- layer 3 ---------------------------------------------------------------------------------
-// Per filter one MFMA i32_16x16x32_i8: A row r = 16-tap band shifted by r (host-built, a3),
-// B column = block of 16 outputs: 32 bytes of the layer-2 row from byte 16 col (output u uses row
-// bytes u+1 .. u+16: pad 7, stored at +8); lane (col, g) loads its aligned 8 bytes.  D lane
-// (col, g) holds outputs 16 col + 4g .. +3 of each of the wave's two filters; the two filters'
-// bytes of one output are adjacent in y3t[u][f] and go out as one 2-byte store.
+// 16-tap depthwise conv (layer3.c:49-79, conv.c:105): output u of filter f reads y2 row bytes
+// u+1 .. u+16 (pad 7, stored at +8), A[r][k] = tap[k - r - 1] over a 32-byte window.  The wave's
+// two filters share MFMA i32_16x16x64_i8 tiles with a block-diagonal K (slots 0..31 filter 0's
+// window and band, 32..63 filter 1's; a lane whose K half belongs to the other filter reads the
+// zero chunk):
+//   tile 1: columns 0..7 = filter 0's blocks of 16 outputs, 8..15 = filter 1's (the first 128
+//           outputs of each; D lane (col, g) holds outputs 16 (col & 7) + 4g .. +3);
+//   tile 2: the L3R outputs past 128 (T8 = 140: 12), four per column: A rows 4g carry shift g and
+//           the other rows are zero, so only register 0 holds results and only it is requantised.
+// The two filters' bytes of one output are adjacent in y3t[u][f]: after requant a lane trades its
+// four bytes with the partner lane col ^ 8 (DPP row_ror:8) and stores two rows as 2-byte pairs.
 template <class K>
 __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, const SmallParams* sp,
                                        const Regs<K>& R, const LaneTab& T, int wave) {
   const float r3 = R.r3, c3 = R.c3;  // wave-uniform (SGPRs): no LDS read per trial
-  unsigned w[FPW];
-#pragma unroll
-  for (int fi = 0; fi < FPW; fi++) {
-    const int f = wave * FPW + fi;
-    const long bv = *(const long*)(smem_y2 + f * K::Y2ROW + T.l3b);
-    // C-init = float magic: acc bits = 1.5 * 2^23 + dot as f32, fma(bits, r, c) == RN(dot * r)
-    v4i acc = {FMAGIC_I, FMAGIC_I, FMAGIC_I, FMAGIC_I};
-    acc = __builtin_amdgcn_mfma_i32_16x16x32_i8(R.a3[fi], bv, acc, 0, 0, 0);
-    // packed here (same-box A/B -0.8 %), plain v_fma_f32 in layer 1 (packed +0.2 %, beside MFMAs)
-    constexpr bool PK3 = true;
-    const f2 q01 = fma2<PK3>(acc[0], acc[1], r3, c3);
-    const f2 q23 = fma2<PK3>(acc[2], acc[3], r3, c3);
-    w[fi] = sat8x4<K::LO>((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
+  const int8_t* y2w = smem_y2 + wave * FPW * K::Y2ROW;
+  // C-init = float magic: acc bits = 1.5 * 2^23 + dot as f32, fma(bits, r, c) == RN(dot * r)
+  const v4i magic = {FMAGIC_I, FMAGIC_I, FMAGIC_I, FMAGIC_I};
+  const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(R.a31, *(const v4i*)(y2w + T.l3b), magic, 0, 0, 0);
+  v4i acc2 = magic, b2 = magic;
+  if constexpr (K::L3RC > 0) {
+    const int* p = (const int*)(y2w + T.l3b2);  // 4-byte aligned
+    b2 = (v4i){p[0], p[1], p[2], p[3]};
+    acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(R.a32, b2, magic, 0, 0, 0);
   }
-  // interleave the two filters: pair i = bytes (f0[i], f1[i])
-  const unsigned p01 = __builtin_amdgcn_perm(w[1], w[0], 0x05010400u);  // f0[0] f1[0] f0[1] f1[1]
-  const unsigned p23 = __builtin_amdgcn_perm(w[1], w[0], 0x07030602u);  // f0[2] f1[2] f0[3] f1[3]
+  const f2 q01 = fma2<true>(acc[0], acc[1], r3, c3);
+  const f2 q23 = fma2<true>(acc[2], acc[3], r3, c3);
+  const unsigned w = sat8x4_b<K::LO>((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
+  const unsigned wp = (unsigned)__builtin_amdgcn_mov_dpp((int)w, 0x128, 0xF, 0xF, false);  // row_ror:8
+  const unsigned pr = __builtin_amdgcn_perm(wp, w, (unsigned)T.l3s);  // (f0, f1) pairs of rows r0, r0+1
   // rows u .. u+3 (u = 16 col + 4 g) share the skew.  Rows T8 .. u+3 of the last block are
   // written too: layer 4 multiplies rows >= T8 only into its discarded outputs (v >= T64).
   if (T.l3w >= 0) {
     int8_t* dst = smem_y3 + T.l3w + FPW * wave;
-    *(unsigned short*)dst = (unsigned short)p01;
-    *(unsigned short*)(dst + K::Y3S) = (unsigned short)(p01 >> 16);
-    *(unsigned short*)(dst + 2 * K::Y3S) = (unsigned short)p23;
-    *(unsigned short*)(dst + 3 * K::Y3S) = (unsigned short)(p23 >> 16);
+    *(unsigned short*)dst = (unsigned short)pr;
+    *(unsigned short*)(dst + K::Y3S) = (unsigned short)(pr >> 16);
+  }
+  if constexpr (K::L3RC > 0) {
+    const int y = min(max((int)__builtin_fmaf(__int_as_float(acc2[0]), r3, c3), K::LO), 127);
+    if (T.l3w2 >= 0) smem_y3[T.l3w2 + FPW * wave] = (int8_t)y;
   }
 }
 

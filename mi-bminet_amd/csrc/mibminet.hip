@@ -303,24 +303,27 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         std::memcpy(&dp.l2t_afrag[w][s][lane], bytes, 16);
       }
   SmallParams& sp = dp.sp;
-  // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed.
-  // A operand of MFMA i32_16x16x32_i8: row r (output shift within a block of 16), K-slot k (byte
-  // 16 col + k of the layer-2 row, which holds position k - 8 + 16 col): output u = 16 col + r
-  // uses bytes u+1 .. u+16, so A[r][k] = tap[k - r - 1].  Lane l holds row l & 15, K-slots
-  // 8 (l >> 4) .. +7.
-  for (int f = 0; f < F2; f++) {
-    int8_t taps[16];
-    for (int j = 0; j < 16; j++) taps[j] = hp.l3_weight[(size_t)f * 16 + 15 - j];
+  // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed.  A
+  // operand of MFMA i32_16x16x64_i8 (forward_wg.hpp, layer3): row r, K-slot k of filter f's half
+  // (byte 16 col + k of its layer-2 row window, which holds position k - 8 + 16 col): output
+  // 16 col + r uses bytes +1 .. +16, so A[r][k] = tap[k - r - 1].  Lane l holds row l & 15,
+  // K-slots 16 (l >> 4) .. +15: groups 0-1 filter 2w, groups 2-3 filter 2w + 1.  Tile 2 carries
+  // shift g on row 4g only.
+  for (int w = 0; w < F2 / 2; w++)
     for (int lane = 0; lane < 64; lane++) {
-      const int r = lane & 15, kg = lane >> 4;
-      int8_t bytes[8];
-      for (int jj = 0; jj < 8; jj++) {
-        const int j = 8 * kg + jj - r - 1;
-        bytes[jj] = (j >= 0 && j < 16) ? taps[j] : 0;
+      const int r = lane & 15, kg = lane >> 4, f = 2 * w + (kg >> 1);
+      int8_t taps[16];
+      for (int j = 0; j < 16; j++) taps[j] = hp.l3_weight[(size_t)f * 16 + 15 - j];
+      int8_t b1[16], b2[16];
+      for (int jj = 0; jj < 16; jj++) {
+        const int k = 16 * (kg & 1) + jj;
+        const int t1 = k - r - 1, t2 = k - r / 4 - 1;
+        b1[jj] = (t1 >= 0 && t1 < 16) ? taps[t1] : 0;
+        b2[jj] = ((r & 3) == 0 && t2 >= 0 && t2 < 16) ? taps[t2] : 0;
       }
-      std::memcpy(&dp.l3_afrag[f][lane], bytes, 8);
+      std::memcpy(&dp.l3_a1[w][lane], b1, 16);
+      std::memcpy(&dp.l3_a2[w][lane], b2, 16);
     }
-  }
   // |layer-3 accumulator| <= 16 * 128 * 128 < 2^22: magic C-init form
   if (!choose_reciprocal(hp.l3_factor, &sp.l3_r, &sp.l3_c, 128, 16LL * A)) return NET_ERR_RANGE;
   // layer 4: B operand of MFMA 32x32x32 = W4^T, block diagonal: lane (column k, half h) holds
