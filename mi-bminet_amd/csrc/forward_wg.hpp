@@ -864,9 +864,11 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     layer1<K>(rc, rn, smem + K::OFF_Y1, R, wave, lane);
     __builtin_amdgcn_s_setprio(0);
     MIB_STAMP(0)
+    // the lane table is read before barrier A, so its LDS latency hides in the barrier wait
+    // instead of delaying layer 2's first loads (same-box A/B -1.8 %)
+    const LaneTab T = ((const LaneTab*)(smem + K::OFF_LT))[ln];
     MIB_LOOP_BARRIER();  // A
     MIB_STAMP(1)
-    const LaneTab T = ((const LaneTab*)(smem + K::OFF_LT))[ln];
 #if MIB_PRIO_L23_LAST
     // the last wave is the youngest of its SIMD: at equal priority it loses the arbitration in
     // layers 2-3 and reaches barrier B last, on the path to its layers 4-5
