@@ -49,6 +49,9 @@ static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wa
 #ifndef MIB_PRIO_L1
 #define MIB_PRIO_L1 1
 #endif
+#ifndef MIB_PRIO_L3
+#define MIB_PRIO_L3 1
+#endif
 #ifndef MIB_PRIO_L45
 #define MIB_PRIO_L45 3
 #endif
@@ -613,6 +616,9 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 #else
   if constexpr (K::TB > 0) {
 #endif
+#if MIB_PRIO_TAIL
+    __builtin_amdgcn_s_setprio(MIB_PRIO_TAIL);  // knob (A/B)
+#endif
     const v4i tacc = layer2_tail_mfma<K>(smem_y1, sp, T, wave, lane);
     layer2_tail_out<K>(tacc, smem_y2, sp, T, wave);
   }
@@ -886,8 +892,17 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #endif
     MIB_STAMP(2)
+#if MIB_PRIO_L3
+    // layer 3 ends the barrier-B interval: at priority 1 a wave's layer 3 wins the arbitration
+    // against the other waves' layer 2 (same-box A/B -1.2 ... -1.6 %; 2: -1.0 %; from the layer-2
+    // tail on: -0.2 %)
+    __builtin_amdgcn_s_setprio(MIB_PRIO_L3);
+#endif
 #ifndef MIB_DIAG_NOL3
     layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, T, wave);
+#endif
+#if MIB_PRIO_L3 && !MIB_PRIO_L3_NORESET
+    __builtin_amdgcn_s_setprio(0);
 #endif
     MIB_STAMP(3)
     MIB_LOOP_BARRIER();  // B
