@@ -45,7 +45,9 @@ constexpr int PF_MAX = MIB_PF_MAX;    // layer-1 blocks per wave prefetched one 
 static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wave");
 // Wave priorities (s_setprio): the last wave's layers 4-5 are the longest dependency chain of the
 // layer-1 interval, so that wave issues first while on them; layer 1 (HBM fragments, next-trial
-// prefetch) goes ahead of the other workgroup's layers 2-3.  Same-box A/B: -4 %.
+// prefetch) goes ahead of the other workgroup's layers 2-3.  Same-box A/B: -4 %.  Layer 3 (the end
+// of the barrier-B interval) at 1 as well: -1.7 %.  MIB_PRIO_TAIL / MIB_PRIO_L23_LAST are A/B knobs
+// (off: both measured slower).
 #ifndef MIB_PRIO_L1
 #define MIB_PRIO_L1 1
 #endif
