@@ -59,9 +59,25 @@ def parse():
     return ap.parse_args()
 
 
+def _cpu_quota():
+    """CPUs granted by the cgroup CPU quota (cgroup v2 cpu.max / v1 cfs), or None if unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(ps, x_dev, seconds):
     """Times the oracle's C restatement of net_model_compute on a bounded sample of the same
-    workload, trials split over the host threads this process may use (rank 0, N = 1 only)."""
+    workload (rank 0, N = 1 only): (ii) all host cores this process may run on (one pthread per
+    CPU of the affinity mask), and (i) one core."""
     sys.path.insert(0, ROOT)
     import oracle  # test infrastructure: only this leg of bench.py may use it
 
@@ -69,9 +85,10 @@ def cpu_baseline(ps, x_dev, seconds):
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
         ncpu = os.cpu_count() or 1
-    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", ncpu)), ncpu, 16))
+    threads = max(1, int(os.environ.get("MIB_CPU_THREADS", ncpu)))
+    quota = _cpu_quota()
     co = oracle.COracle(ps)
-    calib = x_dev[: 32 * threads].cpu().numpy()
+    calib = x_dev[: max(256, 4 * threads)].cpu().numpy()
     t0 = time.perf_counter()
     co.batch(calib, nthreads=threads)
     dt = max(time.perf_counter() - t0, 1e-6)
@@ -93,17 +110,21 @@ def cpu_baseline(ps, x_dev, seconds):
                 break
     except OSError:
         pass
-    # (i) one core as well, on a smaller bounded sample
-    n1 = int(max(8, min(x_dev.shape[0], seconds / 5 / (per_trial * threads))))
+    # (i) one core, on a smaller bounded sample (about a fifth of the time budget)
+    t1 = time.perf_counter()
+    co.batch(calib[:16], nthreads=1)
+    per1 = max(time.perf_counter() - t1, 1e-6) / 16
+    n1 = int(max(16, min(x_dev.shape[0], seconds / 5 / per1)))
     s1 = x_dev[:n1].cpu().numpy()
     t1 = time.perf_counter()
     co.batch(s1, nthreads=1)
     d1 = time.perf_counter() - t1
     return {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
             "sample": f"{n} trials ({reps} pass(es) over the first {n // reps} trials) of the same synthetic batch, C restatement (oracle/oracle.c, -O3) "
-                      f"of net_model_compute, {threads} host threads on {cpu}, {dt:.1f} s",
+                      f"of net_model_compute, {threads} host threads (one per CPU of the affinity mask) on {cpu}, {dt:.1f} s",
             "one_core": {"value": n1 / d1, "unit": "trials/s", "sample": f"{n1} trials, 1 thread, {d1:.1f} s"},
-            "host_cpus": {"affinity": ncpu, "os_cpu_count": os.cpu_count()}}
+            "host_cpus": {"affinity": ncpu, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota,
+                          "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}}
 
 
 def pcie_inclusive(x, y, B, device, sp, stream, reps=5):
@@ -196,14 +217,23 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = ([s.elapsed_time(e) for s, e in ev] if a.per_launch_events
                  else [ev[0][0].elapsed_time(ev[0][1]) / a.steps])
+    rank_avg_ms = float(np.mean(kernel_ms))
+    per_rank = None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed_max = float(t.item())
+        # per-rank record (outside the timed region): which device, its kernel time and its wall time
+        mine = {"rank": rank, "local_rank": local, "device": local, "kernel_ms": rank_avg_ms,
+                "elapsed_s": elapsed, "trials": B}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+        elapsed = elapsed_max
 
     info = lib.launch_info(B, local)
     if rank == 0:
-        avg_kernel_s = float(np.mean(kernel_ms)) / 1e3
+        # N > 1: the slowest rank's kernel average (each rank's is listed under "ranks")
+        avg_kernel_s = (max(r["kernel_ms"] for r in per_rank) if per_rank else rank_avg_ms) / 1e3
         alg_bytes_trial = cfg["C"] * cfg["T"] + 4
         achieved = alg_bytes_trial * B / avg_kernel_s / 1e9
         traffic = None
@@ -239,6 +269,10 @@ def main():
                          "alg_bytes_per_launch": alg_bytes_trial * B},
             "cpu_baseline": None,
         }
+        if dist:
+            out["ranks"] = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
+                            "devices_visible": torch.cuda.device_count(), "per_rank": per_rank,
+                            "note": "each rank times its own shard; value = all ranks' trials / max-over-ranks wall time"}
         if a.pcie:
             out["pcie_inclusive"] = pcie_inclusive(x, y, B, local, sp, stream)
         if world == 1 and not a.no_cpu_baseline:

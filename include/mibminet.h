@@ -81,15 +81,19 @@ int net_last_error(void);
  * reciprocals, and uploads lazily to each device on first use.  Replaces any previous set.  Pad
  * bytes of net_l1_weight_align (channels C..C_ALIGN-1) and of net_l5_weight (columns
  * T64..T64_ALIGN-1 of every row) must be zero, as gen_net_header.py writes them (NET_ERR_BLOB
- * otherwise).  Each distinct set gets its own device copy, which is never overwritten and is kept
- * until the process exits (about 72 KB per set and device): launches already enqueued, and
- * launches captured into a HIP graph, keep running the set (and build variant) they were
- * enqueued with, whatever is loaded later. */
+ * otherwise).  Each distinct set gets its own device copy (about 72 KB per set and device), which
+ * is never overwritten: launches already enqueued, and launches captured into a HIP graph, keep
+ * running the set (and build variant) they were enqueued with, whatever is loaded later.  At most
+ * 8 copies are kept per device: uploading a ninth synchronises the device and frees the least
+ * recently used ones, so a HIP graph that captured a launch with an evicted set must be
+ * re-captured. */
 int net_params_load(const void* blob, size_t len);
 
 /* dims[0..6] = C, T, F1, F2, N, weight_bits, loaded(0/1). */
 int net_params_dims(int32_t* dims);
 
+/* Drops the loaded set and frees every device copy of every set, after synchronising each device
+ * that holds copies (HIP graphs capturing launches must be dropped first). */
 void net_params_unload(void);
 
 /* ---- batched device entry points ---------------------------------------------------------- */
@@ -120,7 +124,7 @@ int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* co
  * ([B][stride], stride = C*T rounded up to 16, each trial [T][C], pad bytes zero), computed as
  * trunc(clip(x / scale, -1, 1) * 127) in the input's precision.  scale = absMaxValue of the
  * network's quant1 activation.  Enqueued on `stream` (NULL = null stream), no host sync.
- * B <= 65535 per call. */
+ * Any B up to INT32_MAX in one call (batches past 65,535 trials loop inside the kernel). */
 int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, float scale, int device,
                            void* stream);
 int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, double scale, int device,
@@ -135,7 +139,7 @@ int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int de
 
 /* Already-quantised int8 trials in channel-major [B][C][T] (the layout of the reference's
  * input.npz, transposed by gen_input_header.py:74 on the host): the same GPU transpose into the
- * batched [B][stride] layout, without the quantisation.  DEVICE pointers, B <= 65535 per call,
+ * batched [B][stride] layout, without the quantisation.  DEVICE pointers, B <= INT32_MAX,
  * C <= 64, enqueued on `stream`, no host sync. */
 int net_pack_trials_i8(const int8_t* x, int8_t* y, size_t B, int C, int T, int device, void* stream);
 

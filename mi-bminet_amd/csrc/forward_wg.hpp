@@ -137,7 +137,7 @@ struct Cfg {
   // LDS carve
   static constexpr int OFF_Y1 = 0;
   static constexpr int OFF_Y2 = OFF_Y1 + F2 * Y1ROW;
-  static constexpr int OFF_Y3 = OFF_Y2 + align16(F2 * Y2ROW) + 256;  // layer-3 reads may run 256 B past
+  static constexpr int OFF_Y3 = OFF_Y2 + align16(F2 * Y2ROW);  // layer 3 reads only inside the wave's y2 rows
   static constexpr int OFF_Y4 = OFF_Y3 + align16(Y3ROWS * Y3S + 4 * (Y3ROWS >> 4));
   static constexpr int OFF_SP = OFF_Y4 + align16(64 * N5L);
   static constexpr int OFF_LT = align16(OFF_SP + (int)sizeof(SmallParams));   // per-lane offsets
@@ -697,8 +697,10 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
   const unsigned w = sat8x4_b<K::LO>((int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]);
   const unsigned wp = (unsigned)__builtin_amdgcn_mov_dpp((int)w, 0x128, 0xF, 0xF, false);  // row_ror:8
   const unsigned pr = __builtin_amdgcn_perm(wp, w, (unsigned)T.l3s);  // (f0, f1) pairs of rows r0, r0+1
-  // rows u .. u+3 (u = 16 col + 4 g) share the skew.  Rows T8 .. u+3 of the last block are
-  // written too: layer 4 multiplies rows >= T8 only into its discarded outputs (v >= T64).
+  // rows u .. u+3 (u = 16 col + 4 g) share the skew.  Tile 1 writes whole blocks of 16 rows, so
+  // rows T8 .. 16 L3C - 1 are written too when T8 < 16 L3C (64 x 1000: 125..127, 64 x 480: 60..63):
+  // layer 4 multiplies rows >= T8 only into its discarded outputs (v >= T64).  Tile 2 stores only
+  // rows < T8 (LaneTab::l3w2).
   if (T.l3w >= 0) {
     int8_t* dst = smem_y3 + T.l3w + FPW * wave;
     *(unsigned short*)dst = (unsigned short)pr;

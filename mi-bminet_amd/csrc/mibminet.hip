@@ -397,18 +397,25 @@ size_t trial_stride(const Dims& d) { return ((size_t)d.C * d.T + 15) / 16 * 16; 
 // ---- global state --------------------------------------------------------------------------
 // One device copy of the parameter image per loaded generation: a load never overwrites a copy
 // that a kernel may still read, so launches in flight and launches captured into a HIP graph keep
-// the image (and with it the compiled variant) they were enqueued with.  Copies are released only
-// at process exit; a reload of a byte-identical image reuses its copy.
+// the image (and with it the compiled variant) they were enqueued with.  A reload of a
+// byte-identical image reuses its copy.  The copies per device are bounded: when a new image would
+// make more than MAX_IMAGES, the device is synchronised (no launch still reads an old copy) and
+// the least recently used copies are freed; net_params_unload frees every copy the same way.  A
+// HIP graph that captured a launch with an evicted image must be re-captured.
+constexpr size_t MAX_IMAGES = 8;
+
 struct DevImage {
   std::shared_ptr<const DevParams> host;  // what was uploaded
   DevParams* dev = nullptr;
+  uint64_t used = 0;                      // DeviceState::tick at the last selection
 };
 
 struct DeviceState {
   std::mutex mu;
   uint64_t gen = 0;             // params generation of `cur`
   DevParams* cur = nullptr;     // device copy of that generation
-  std::vector<DevImage> images; // every copy uploaded to this device
+  std::vector<DevImage> images; // the copies uploaded to this device (at most MAX_IMAGES)
+  uint64_t tick = 0;
   int8_t* d_in = nullptr;       // single-trial scratch
   int8_t* d_out = nullptr;
   size_t scratch = 0;
@@ -468,14 +475,27 @@ int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
     ds.cus = cus;
   }
   if (ds.gen != s.gen || !ds.cur) {
-    for (const DevImage& im : ds.images)  // a set loaded before: its copy is still there, unchanged
+    for (DevImage& im : ds.images)  // a set loaded before: its copy is still there, unchanged
       if (im.host == s.dev || std::memcmp(im.host.get(), s.dev.get(), sizeof(DevParams)) == 0) {
         ds.cur = im.dev;
         ds.gen = s.gen;
+        im.used = ++ds.tick;
         return NET_OK;
       }
+    if (ds.images.size() >= MAX_IMAGES) {
+      // evict the least recently used copies once every launch on the device has finished
+      hipError_t e = hipDeviceSynchronize();
+      if (e != hipSuccess) return hip_err(e);
+      std::sort(ds.images.begin(), ds.images.end(),
+                [](const DevImage& a, const DevImage& b) { return a.used > b.used; });
+      while (ds.images.size() >= MAX_IMAGES) {
+        (void)hipFree(ds.images.back().dev);
+        ds.images.pop_back();
+      }
+    }
     DevImage im;
     im.host = s.dev;
+    im.used = ++ds.tick;
     hipError_t e = hipMalloc((void**)&im.dev, sizeof(DevParams));
     if (e != hipSuccess) return hip_err(e);
     e = hipMemcpy(im.dev, s.dev.get(), sizeof(DevParams), hipMemcpyHostToDevice);
@@ -589,14 +609,15 @@ template <class F>
 int quantize_input(const F* x, int8_t* y, size_t B, int C, int T, F scale, int device, void* stream) {
   if ((!x || !y) && B) return NET_ERR_INVALID;
   if (C < 1 || C > quant::CMAX || T < 1 || device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
-  if (B > 65535 || !(scale > 0)) return NET_ERR_INVALID;
+  if (B > (size_t)INT32_MAX || !(scale > 0)) return NET_ERR_INVALID;
   if (B == 0) return NET_OK;
   if (const int rc = check_device(device)) return rc;
   const int stride = (int)(((size_t)C * T + 15) / 16 * 16);
   DeviceGuard guard(device);
   if (guard.err != hipSuccess) return hip_err(guard.err);
-  dim3 grid((T + quant::TT - 1) / quant::TT, (unsigned)B);
-  hipLaunchKernelGGL(quant::k_quantize<F>, grid, dim3(quant::QTHREADS), 0, (hipStream_t)stream, x, y, C, T, stride, scale);
+  dim3 grid((T + quant::TT - 1) / quant::TT, (unsigned)std::min(B, (size_t)quant::YMAX));
+  hipLaunchKernelGGL(quant::k_quantize<F>, grid, dim3(quant::QTHREADS), 0, (hipStream_t)stream, x, y, C, T, stride, scale,
+                     (int)B);
   return hip_err(hipGetLastError());
 }
 
@@ -649,10 +670,23 @@ int net_params_load(const void* blob, size_t len) {
 }
 
 void net_params_unload(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  g_host.reset();
-  g_dev.reset();
-  g_gen++;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_host.reset();
+    g_dev.reset();
+    g_gen++;
+  }
+  // free every device copy once the launches that may read it have finished
+  for (int d = 0; d < MAX_DEVICES; d++) {
+    DeviceState& ds = g_devs[d];
+    std::lock_guard<std::mutex> lk(ds.mu);
+    if (ds.images.empty()) continue;
+    DeviceGuard guard(d);
+    if (guard.err != hipSuccess || hipDeviceSynchronize() != hipSuccess) continue;  // keep them
+    for (DevImage& im : ds.images) (void)hipFree(im.dev);
+    ds.images.clear();
+    ds.cur = nullptr;
+  }
 }
 
 int net_params_dims(int32_t* dims) {

@@ -8,7 +8,8 @@
 //                                                           to nearest in that precision)
 // (* 254 then / 2 equals * 127 exactly: scaling by 2 commutes with rounding.)
 //
-// HBM-bound streaming transpose: one workgroup per (64-sample time tile, trial); reads the
+// HBM-bound streaming transpose: one workgroup per (64-sample time tile, trial; batches past
+// 65,535 trials loop over trials in the workgroup); reads the
 // C rows of the tile coalesced along time, quantises, transposes through LDS and writes the
 // tile's 64 * C output bytes as contiguous dwords.  The trial's pad bytes (stride - C * T) are
 // written as zeros by the last tile.
@@ -22,6 +23,7 @@ namespace quant {
 constexpr int TT = 64;          // time samples per tile
 constexpr int QTHREADS = 256;
 constexpr int CMAX = 64;
+constexpr int YMAX = 65535;   // grid.y limit: trials per launch row (larger batches loop)
 
 template <class F>
 __device__ __forceinline__ int quantize_one(F x, F s);
@@ -49,32 +51,35 @@ __device__ __forceinline__ int quantize_one<int8_t>(int8_t x, int8_t) {
 
 template <class F>
 __global__ __launch_bounds__(QTHREADS) void k_quantize(const F* __restrict__ x, int8_t* __restrict__ y,
-                                                       int C, int T, int stride, F s) {
+                                                       int C, int T, int stride, F s, int B) {
   __shared__ __attribute__((aligned(16))) int8_t tile[TT * CMAX];
-  const int b = blockIdx.y;
   const int t0 = blockIdx.x * TT;
   const int nt = min(TT, T - t0);
-  const F* xb = x + (size_t)b * C * T;
-  // read: consecutive threads walk time within a channel row (coalesced)
-  for (int i = threadIdx.x; i < C * TT; i += QTHREADS) {
-    const int c = i / TT, t = i - c * TT;
-    if (t < nt) tile[t * C + c] = (int8_t)quantize_one<F>(xb[(size_t)c * T + t0 + t], s);
-  }
-  __syncthreads();
-  // write: the tile's nt * C bytes are contiguous in the output; dwords when aligned
-  int8_t* yb = y + (size_t)b * stride + (size_t)t0 * C;
-  const int nbytes = nt * C;
-  if (((t0 * C) & 3) == 0) {
-    const int nd = nbytes >> 2;
-    for (int i = threadIdx.x; i < nd; i += QTHREADS) ((int*)yb)[i] = ((const int*)tile)[i];
-    for (int i = (nd << 2) + threadIdx.x; i < nbytes; i += QTHREADS) yb[i] = tile[i];
-  } else {
-    for (int i = threadIdx.x; i < nbytes; i += QTHREADS) yb[i] = tile[i];
-  }
-  // trial pad bytes
-  if (t0 + TT >= T) {
-    int8_t* pad = y + (size_t)b * stride + (size_t)C * T;
-    for (int i = threadIdx.x; i < stride - C * T; i += QTHREADS) pad[i] = 0;
+  // trials: grid.y is capped at YMAX, so a workgroup walks trials blockIdx.y + k gridDim.y
+  for (int b = blockIdx.y; b < B; b += gridDim.y) {
+    const F* xb = x + (size_t)b * C * T;
+    if (b != (int)blockIdx.y) __syncthreads();  // the previous trial's tile has been written out
+    // read: consecutive threads walk time within a channel row (coalesced)
+    for (int i = threadIdx.x; i < C * TT; i += QTHREADS) {
+      const int c = i / TT, t = i - c * TT;
+      if (t < nt) tile[t * C + c] = (int8_t)quantize_one<F>(xb[(size_t)c * T + t0 + t], s);
+    }
+    __syncthreads();
+    // write: the tile's nt * C bytes are contiguous in the output; dwords when aligned
+    int8_t* yb = y + (size_t)b * stride + (size_t)t0 * C;
+    const int nbytes = nt * C;
+    if (((t0 * C) & 3) == 0) {
+      const int nd = nbytes >> 2;
+      for (int i = threadIdx.x; i < nd; i += QTHREADS) ((int*)yb)[i] = ((const int*)tile)[i];
+      for (int i = (nd << 2) + threadIdx.x; i < nbytes; i += QTHREADS) yb[i] = tile[i];
+    } else {
+      for (int i = threadIdx.x; i < nbytes; i += QTHREADS) yb[i] = tile[i];
+    }
+    // trial pad bytes
+    if (t0 + TT >= T) {
+      int8_t* pad = y + (size_t)b * stride + (size_t)C * T;
+      for (int i = threadIdx.x; i < stride - C * T; i += QTHREADS) pad[i] = 0;
+    }
   }
 }
 

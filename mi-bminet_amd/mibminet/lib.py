@@ -266,10 +266,7 @@ def quantize_input_torch(x, scale: float, stream=None):
     y = torch.empty((B, stride), dtype=torch.int8, device=x.device)
     s = torch.cuda.current_stream(x.device) if stream is None else stream
     fn = load().net_quantize_input_f32 if x.dtype == torch.float32 else load().net_quantize_input_f64
-    for lo in range(0, B, 65535):
-        n = min(65535, B - lo)
-        _check(fn(x[lo:].data_ptr(), y[lo:].data_ptr(), n, C, T, scale, x.device.index or 0, s.cuda_stream),
-               "net_quantize_input")
+    _check(fn(x.data_ptr(), y.data_ptr(), B, C, T, scale, x.device.index or 0, s.cuda_stream), "net_quantize_input")
     return y
 
 
@@ -299,10 +296,8 @@ def pack_trials_torch(x, stream=None):
     stride = (C * T + 15) // 16 * 16
     y = torch.empty((B, stride), dtype=torch.int8, device=x.device)
     s = torch.cuda.current_stream(x.device) if stream is None else stream
-    for lo in range(0, B, 65535):
-        n = min(65535, B - lo)
-        _check(load().net_pack_trials_i8(x[lo:].data_ptr(), y[lo:].data_ptr(), n, C, T, x.device.index or 0,
-                                         s.cuda_stream), "net_pack_trials_i8")
+    _check(load().net_pack_trials_i8(x.data_ptr(), y.data_ptr(), B, C, T, x.device.index or 0, s.cuda_stream),
+           "net_pack_trials_i8")
     return y
 
 

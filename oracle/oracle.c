@@ -42,6 +42,14 @@ int32_t or_func_dotp(const int8_t* a, const int8_t* b, unsigned len) {
 
 static inline int32_t dotp(const int8_t* a, const int8_t* b, int len) { return or_func_dotp(a, b, (unsigned)len); }
 
+/* func_dotp_slow (dotp.c:172-210): scalar dot product over strided vectors, sum_i a[i as] b[i bs]
+ * (two interleaved accumulators in the reference; the same int32 sum) */
+int32_t or_func_dotp_slow(const int8_t* a, unsigned as, const int8_t* b, unsigned bs, unsigned len) {
+    int32_t acc = 0;
+    for (unsigned i = 0; i < len; i++) acc += (int32_t)a[(size_t)i * as] * (int32_t)b[(size_t)i * bs];
+    return acc;
+}
+
 /* The longer vector is the signal (xcorr.c:44-57, conv.c:67-80 swap a and b when a is shorter). */
 static void order_ab(const int8_t** a, unsigned* la, const int8_t** b, unsigned* lb) {
     if (*la < *lb) {
@@ -228,6 +236,34 @@ void or_layer4(const or_params_t* p, const int8_t* y3t, int8_t* y4) {
             } else {
                 sum = sum >> 3;  /* layer4.c:130 */
             }
+            y4[(size_t)k * p->T64_ALIGN + v] = (int8_t)clipq(p, sum);
+        }
+    }
+}
+
+/* Layer 4 without FLIP_LAYERS: layer4.c:380-505.  The same arithmetic as or_layer4 on the
+ * unflipped [F2][T8_ALIGN] layer-3 output: each element is func_dotp_slow down a column (stride
+ * T8_ALIGN) against the weight row.  A second restatement of layer 4 from the reference's other
+ * build branch, used to cross-check or_layer4 (tests/test_oracle_func.py). */
+void or_layer4_noflip(const or_params_t* p, const int8_t* y3, int8_t* y4) {
+    memset(y4, 0, (size_t)p->F2 * p->T64_ALIGN);
+    for (int k = 0; k < p->F2; k++) {
+        int32_t fac = p->l4_factor[k], off = p->l4_offset[k], thr = 0;
+        if (p->reorder_bn) thr = -(off >> 3);
+        else { fac = fac >> 3; off = off >> 3; }
+        const int8_t* w = p->l4_weight + (size_t)k * p->F2;
+        const int8_t* it = y3;
+        for (int v = 0; v < p->T64; v++) {
+            int32_t sum = 0;
+            for (int i = 0; i < 8; i++) {
+                int32_t e = or_func_dotp_slow(it, (unsigned)p->T8_ALIGN, w, 1, (unsigned)p->F2);
+                if (p->reorder_bn) e = e > thr ? e : thr;
+                else { e = (e + off) / fac; e = e > 0 ? e : 0; }
+                sum += e;
+                it += 1;
+            }
+            if (p->reorder_bn) sum = (sum + off) / fac;
+            else sum = sum >> 3;
             y4[(size_t)k * p->T64_ALIGN + v] = (int8_t)clipq(p, sum);
         }
     }

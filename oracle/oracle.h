@@ -54,6 +54,7 @@ typedef struct {
 } or_params_t;
 
 /* func primitives (src/cl/func/{dotp,xcorr,conv,transform,flip}.c), clip to [-128, 127] as the C's __CLIP_R */
+int32_t or_func_dotp_slow(const int8_t* a, unsigned as, const int8_t* b, unsigned bs, unsigned len);
 int32_t or_func_dotp(const int8_t* a, const int8_t* b, unsigned len);
 void or_func_xcorr(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t* r);
 void or_func_xcorr_scale(const int8_t* a, unsigned la, const int8_t* b, unsigned lb, int32_t div, int32_t offset,
@@ -72,6 +73,8 @@ void or_layer3(const or_params_t* p, const int8_t* y2, int8_t* y3);
 void or_layer3_flip_inplace(const or_params_t* p, int8_t* y3);
 void or_layer4(const or_params_t* p, const int8_t* y3t, int8_t* y4);
 void or_layer5(const or_params_t* p, const int8_t* y4, int8_t* out);
+/* layer 4 of the non-FLIP_LAYERS build (layer4.c:380-505) on the unflipped [F2][T8_ALIGN] input */
+void or_layer4_noflip(const or_params_t* p, const int8_t* y3, int8_t* y4);
 
 /* net_model_compute restated (model.c:84-148); x is [T][C_ALIGN]. */
 void or_model_compute(const or_params_t* p, const int8_t* x, int8_t* out);

@@ -35,26 +35,56 @@ def test_device_index_past_count(gpu):
 
 
 def test_multi_error_waits_for_enqueued_shards(gpu):
+    """On an error, net_model_compute_batch_multi returns only after the shards enqueued before
+    the failing one have finished.  Checked without any synchronising call: right after the call
+    the stream shard 0 ran on must already be idle (stream query), which fails if the wait is
+    removed (shard 0 is a full 65,536-trial launch, ~0.4 ms, far longer than the call's return)."""
     import torch
 
     L = lib.load()
     ps = ParamSet.synthetic(seed=62)
     lib.params_load(ps)
-    rng = np.random.default_rng(62)
-    x = pack_trials(rng.integers(-128, 128, size=(3000, 22, 1125)))
-    want = oracle.COracle(ps).batch(x, nthreads=8)
+    B = 65536
     stride = lib.trial_stride()
-    xd = torch.from_numpy(x).cuda()
-    y0 = torch.zeros((3000, 4), dtype=torch.int8, device=gpu)
+    g = torch.Generator(device="cuda").manual_seed(62)
+    xd = torch.randint(-128, 128, (B, stride), dtype=torch.int8, device=gpu, generator=g)
+    xd[:, 22 * 1125:] = 0
+    y0 = torch.zeros((B, 4), dtype=torch.int8, device=gpu)
     raw = torch.zeros(16 + 4 * 4, dtype=torch.int8, device=gpu)
-    for streams in (None, [torch.cuda.current_stream().cuda_stream] * 2):
+    idx = np.random.default_rng(62).choice(B, 256, replace=False)
+    want = oracle.COracle(ps).batch(xd[torch.from_numpy(idx).cuda()].cpu().numpy(), nthreads=8)
+    side = torch.cuda.Stream(device=gpu)
+    torch.cuda.synchronize()
+    for mode in ("null", "side"):
         y0.zero_()
+        torch.cuda.synchronize()
         dev = (ctypes.c_int * 2)(0, 0)
         xp = (ctypes.c_void_p * 2)(xd.data_ptr(), xd.data_ptr() + 1)  # shard 1 misaligned
         yp = (ctypes.c_void_p * 2)(y0.data_ptr(), raw.data_ptr())
-        bs = (ctypes.c_size_t * 2)(3000, 4)
-        sp = None if streams is None else (ctypes.c_void_p * 2)(*streams)
+        bs = (ctypes.c_size_t * 2)(B, 4)
+        st = torch.cuda.default_stream(gpu) if mode == "null" else side
+        sp = None if mode == "null" else (ctypes.c_void_p * 2)(side.cuda_stream, side.cuda_stream)
         assert L.net_model_compute_batch_multi(2, dev, xp, yp, bs, sp) == lib.NET_ERR_INVALID
+        # no sync before this: shard 0's stream must be idle already
+        assert st.query(), f"{mode}: shard 0 still running when the error was returned"
+        torch.cuda.synchronize()
         # shard 0, enqueued before the failing shard, ran to completion
-        assert np.array_equal(y0.cpu().numpy(), want)
-        assert stride % 16 == 0
+        assert np.array_equal(y0.cpu().numpy()[idx], want)
+    assert stride % 16 == 0
+
+
+def test_param_images_bounded_and_reloadable(gpu):
+    """12 distinct parameter sets in turn (more than the 8 device copies kept): every launch uses
+    its own set, an evicted set reloads correctly, and unload + load works."""
+    import torch
+
+    rng = np.random.default_rng(70)
+    x = pack_trials(rng.integers(-128, 128, size=(8, 22, 1125)))
+    xd = torch.from_numpy(x).cuda()
+    sets = [ParamSet.synthetic(seed=700 + i) for i in range(12)]
+    for ps in sets + sets[:2]:
+        lib.params_load(ps)
+        assert np.array_equal(lib.forward_torch(xd).cpu().numpy(), oracle.COracle(ps).batch(x, nthreads=4))
+    lib.params_unload()
+    lib.params_load(sets[5])
+    assert np.array_equal(lib.forward_torch(xd).cpu().numpy(), oracle.COracle(sets[5]).batch(x, nthreads=4))

@@ -129,3 +129,45 @@ def test_flip(outer, inner):
     r = np.full((inner, oa), 0x55, np.int8)
     _L().or_func_flip_2d_axis(_p(xin), outer, inner, _p(r))
     assert np.array_equal(r, want)
+
+
+@pytest.mark.parametrize("length", [22, 23, 1024, 1025])  # dotp_slow/testcase.py:66-67
+@pytest.mark.parametrize("a_stride,b_stride", [(1, 1), (4, 1), (8, 4)])
+def test_dotp_slow(length, a_stride, b_stride):
+    """func_dotp_slow (dotp.c:172): the test's [length][stride] arrays, expectation
+    np.dot(vec_a[:, 0], vec_b[:, 0])."""
+    L = _L()
+    L.or_func_dotp_slow.argtypes = [vp, u, vp, u, u]
+    L.or_func_dotp_slow.restype = i32
+    rng = np.random.default_rng(length * 100 + a_stride * 10 + b_stride)
+    a = rng.integers(-128, 127, size=(length, a_stride)).astype(np.int8)
+    b = rng.integers(-128, 127, size=(length, b_stride)).astype(np.int8)
+    want = int(np.dot(a[:, 0].astype(np.int64), b[:, 0].astype(np.int64)))
+    assert L.or_func_dotp_slow(_p(a), a_stride, _p(b), b_stride, length) == want
+
+
+@pytest.mark.parametrize("C,T,stress,reorder", [(22, 1125, False, True), (22, 1125, True, True),
+                                                (64, 1000, True, True), (22, 1125, True, False)])
+def test_layer4_flip_and_noflip_branches_agree(C, T, stress, reorder):
+    """Layer 4 restated twice, from the reference's two build branches: FLIP_LAYERS (layer4.c:51-149,
+    dotp over rows of the flipped [T8][F2] input: or_layer4) and without it (layer4.c:380-505,
+    func_dotp_slow down the columns of the unflipped [F2][T8_ALIGN] input: or_layer4_noflip).  They
+    must agree on every output, including both clip rails and negative truncation (stress params)."""
+    from mibminet.params import ParamSet
+
+    ps = ParamSet.synthetic(seed=C + T + stress, C=C, T=T, stress=stress, reorder_bn=reorder)
+    co = oracle.COracle(ps)
+    L = co.L
+    L.or_layer4_noflip.argtypes = [vp, vp, vp]
+    L.or_layer4_noflip.restype = None
+    d = ps.dims
+    rng = np.random.default_rng(C * T)
+    for trial in range(6):
+        lo, hi = [(-128, 128), (-60, 60), (-128, -100), (100, 128), (-8, 8), (-128, 128)][trial]
+        y3 = np.zeros((d.F2, d.T8_ALIGN), np.int8)
+        y3[:, : d.T8] = rng.integers(lo, hi, size=(d.F2, d.T8))
+        flipped = co.layer3_flip(y3)
+        a = co.layer4(flipped)
+        b = np.empty((d.F2, d.T64_ALIGN), np.int8)
+        L.or_layer4_noflip(co.pref, y3.ctypes.data, b.ctypes.data)
+        np.testing.assert_array_equal(a[:, : d.T64], b[:, : d.T64])

@@ -97,7 +97,7 @@ def test_pack_abi_checks():
     assert L.net_pack_trials_i8(None, None, 1, 22, 1125, 0, None) == lib.NET_ERR_INVALID
     buf = np.zeros(64, np.int8)
     assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 1, 65, 10, 0, None) == lib.NET_ERR_INVALID
-    assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 65536, 22, 1125, 0, None) == lib.NET_ERR_INVALID
+    assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 2**31, 22, 1125, 0, None) == lib.NET_ERR_INVALID
 
 
 @pytest.mark.gpu
@@ -128,3 +128,44 @@ def test_gpu_int8_channel_major_end_to_end(gpu):
     x = rng.integers(-128, 128, size=(257, 22, 1125)).astype(np.int8)
     y = lib.forward_torch(lib.pack_trials_torch(torch.from_numpy(x).to("cuda:0"))).cpu().numpy()
     assert np.array_equal(y, oracle.COracle(ps).batch(pack_trials(x), nthreads=4))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_gpu_quantize_past_grid_limit(gpu, dtype):
+    """B = 100,000 in one call (more trials than grid.y's 65,535: the kernel loops over trials)
+    == the NumPy restatement, for every trial."""
+    import torch
+    from mibminet import lib
+
+    B, C, T, s = 100_000, 5, 70, 0.93
+    rng = np.random.default_rng(100)
+    x = rng.normal(scale=0.7, size=(B, C, T)).astype(dtype)
+    got = lib.quantize_input_torch(torch.from_numpy(x).to("cuda:0"), s).cpu().numpy()
+    assert np.array_equal(got, G.quantize_input(x, s))
+    xi = rng.integers(-128, 128, size=(B, C, T)).astype(np.int8)
+    from mibminet.params import pack_trials
+    assert np.array_equal(lib.pack_trials_torch(torch.from_numpy(xi).to("cuda:0")).cpu().numpy(), pack_trials(xi))
+
+
+@pytest.mark.gpu
+def test_gpu_float_path_config_b_100k(gpu):
+    """Config-B float trials, B = 100,000 in one quantiser call (device-generated input), then the
+    forward: sampled trials (random and the last 64) equal oracle(quantize_input(x))."""
+    import torch
+    import oracle
+    from mibminet import lib
+    from mibminet.params import ParamSet
+
+    B = 100_000
+    ps = ParamSet.synthetic(seed=13)
+    lib.params_load(ps)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.randn((B, 22, 1125), dtype=torch.float32, device="cuda", generator=g) * 0.8
+    xq = lib.quantize_input_torch(x, 1.1)
+    y = lib.forward_torch(xq).cpu().numpy()
+    idx = np.concatenate([np.random.default_rng(2).choice(B - 64, 128, replace=False), np.arange(B - 64, B)])
+    xs = x[torch.from_numpy(idx).cuda()].cpu().numpy()
+    want_q = G.quantize_input(xs, 1.1)
+    assert np.array_equal(xq[torch.from_numpy(idx).cuda()].cpu().numpy(), want_q)
+    assert np.array_equal(y[idx], oracle.COracle(ps).batch(want_q, nthreads=8))

@@ -5,90 +5,193 @@
   dst partially over srcA/B  vdst overlaps a multiplicand of the same instruction without being it
   asm write into pending dst an inline-asm instruction (between ;;#ASMSTART and ;;#ASMEND) writes a
                              register of an earlier MFMA's destination that nothing has read yet:
-                             the compiler's hazard checks do not see inline asm, and the MFMA's
-                             write-back can land after the asm result (the round-2 layer-3 fault)
+                             the MFMA's write-back can land after the asm result (WAW; the
+                             round-2 layer-3 fault)
+  asm write into srcC (WAR)  an inline-asm instruction writes a register that an MFMA issued fewer
+                             than W wait states earlier reads as srcC.  A multi-pass MFMA reads
+                             srcC late, so the write can reach the accumulator's C-init (the
+                             round-1 layer-1 fault).  srcA/srcB are read at issue
+                             and have no such window.
+
+Why inline asm: the compiler's hazard recognizer inserts the required wait states (s_nop) for every
+instruction it emitted itself, but it cannot see into inline asm, so neither the WAR nor the WAW
+window is guarded there.
+
+Wait states W are the compiler's own (GCNHazardRecognizer, gfx940 family), confirmed on the
+ROCm 7.2 compiler by probes that overwrite srcC right after an MFMA (it inserts exactly 3 wait
+states for v_mfma_i32_16x16x64_i8): 4-pass XDL 3, 8-pass 7, 16-pass 15.  The tool uses the pass
+count itself (one more than the compiler) as the window.
+
+Control flow: each MFMA is followed along every path of the function (fall-through, s_branch
+targets, both sides of s_cbranch_*), so a hazard across a loop back edge or a branch is seen.
+The walk stops once the WAR window has passed and every destination register has been read or
+overwritten (or after 400 instructions on a path).
 
 usage: python tools/mfma_lint.py mi-bminet_amd/build/mibminet.s
 """
 import re
 import sys
 
+# passes (4 cycles each) of the MFMAs this kernel uses on gfx950
+PASSES = {
+    "v_mfma_i32_16x16x64_i8": 4,
+    "v_mfma_i32_32x32x32_i8": 8,
+    "v_mfma_i32_16x16x32_i8": 4,
+    "v_mfma_i32_32x32x16_i8": 8,
+}
+DEFAULT_PASSES = 16  # unknown shape: assume the longest
+
 
 def rng(tok):
     tok = tok.strip().rstrip(",")
-    m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
+    m = re.fullmatch(r"([va])\[(\d+):(\d+)\]", tok)
     if m:
-        return int(m.group(1)), int(m.group(2))
-    m = re.fullmatch(r"v(\d+)", tok)
+        return m.group(1), int(m.group(2)), int(m.group(3))
+    m = re.fullmatch(r"([va])(\d+)", tok)
     if m:
-        return int(m.group(1)), int(m.group(1))
+        return m.group(1), int(m.group(2)), int(m.group(2))
     return None
-
-
-def ov(a, b):
-    return a and b and not (a[1] < b[0] or b[1] < a[0])
 
 
 def regs(tok):
     r = rng(tok)
-    return set(range(r[0], r[1] + 1)) if r else set()
+    return {(r[0], i) for i in range(r[1], r[2] + 1)} if r else set()
 
 
-bad = 0
-fn = None
-lines = open(sys.argv[1]).read().split("\n")
-# pass 1: inline-asm writes into MFMA destination registers that are still unread
-in_asm = False
-pending = {}  # reg -> line of the MFMA that writes it
-for i, line in enumerate(lines):
-    s = line.strip()
-    if re.match(r"^_Z\S+:", s):
-        fn = s.split(":")[0]
-        pending = {}
-    if s.startswith(";;#ASMSTART"):
-        in_asm = True
-        continue
-    if s.startswith(";;#ASMEND"):
-        in_asm = False
-        continue
-    if not s or s.startswith(";") or s.startswith(".") or s.endswith(":"):
-        continue
-    parts = s.split(None, 1)
-    op = parts[0]
-    ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
-    srcs = set().union(*(regs(o.split()[0]) for o in ops[1:] if o)) if len(ops) > 1 else set()
-    if op.startswith(("ds_write", "global_store", "buffer_store", "scratch_store")):
-        srcs |= set().union(*(regs(o.split()[0]) for o in ops if o)) if ops else set()
-        dst = set()
-    else:
-        dst = regs(ops[0].split()[0]) if ops and op.startswith(("v_", "ds_read", "global_load", "buffer_load")) else set()
-    for r in srcs:
-        pending.pop(r, None)
-    if op.startswith("v_mfma"):
-        for r in dst:
-            pending[r] = i + 1
-        continue
-    hit = dst & set(pending)
-    if hit and in_asm:
-        bad += 1
-        print(f"{i + 1}: {s}    <- asm write into pending dst of the MFMA at line {pending[min(hit)]}  [{fn[:60] if fn else '?'}]")
-    for r in dst:
-        pending.pop(r, None)
-fn = None
-for i, line in enumerate(lines):
-    s = line.strip()
-    if re.match(r"^_Z\S+:", s):
-        fn = s.split(":")[0]
-    if not s.startswith("v_mfma"):
-        continue
-    ops = [o.strip() for o in s.split(None, 1)[1].split(",")]
-    d, a, b, c = (rng(o) for o in ops[:4])
-    why = []
-    if ov(d, c) and d != c:
-        why.append("partial dst/srcC overlap")
-    if (ov(d, a) and d != a) or (ov(d, b) and d != b):
-        why.append("dst partially over srcA/srcB")
-    if why:
-        bad += 1
-        print(f"{i + 1}: {s}    <- {', '.join(why)}  [{fn[:60] if fn else '?'}]")
-print(f"{bad} suspect MFMA(s)")
+def ov(a, b):
+    return a and b and a[0] == b[0] and not (a[2] < b[1] or b[2] < a[1])
+
+
+class Ins:
+    __slots__ = ("line", "text", "op", "ops", "asm", "dst", "src")
+
+    def __init__(self, line, text, asm):
+        self.line, self.text, self.asm = line, text, asm
+        parts = text.split(None, 1)
+        self.op = parts[0]
+        self.ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
+        first = lambda o: o.split()[0] if o else ""  # noqa: E731
+        op = self.op
+        if op.startswith(("ds_write", "global_store", "buffer_store", "scratch_store", "flat_store")):
+            self.dst = set()
+            self.src = set().union(set(), *(regs(first(o)) for o in self.ops))
+        elif op.startswith(("v_", "ds_read", "global_load", "buffer_load", "scratch_load", "flat_load")):
+            self.dst = regs(first(self.ops[0])) if self.ops else set()
+            self.src = set().union(set(), *(regs(first(o)) for o in self.ops[1:]))
+        else:
+            self.dst = set()
+            self.src = set().union(set(), *(regs(first(o)) for o in self.ops))
+
+    def wait_states(self):
+        if self.op == "s_nop":
+            try:
+                return int(self.ops[0], 0) + 1
+            except (ValueError, IndexError):
+                return 1
+        return 1
+
+
+def parse(lines):
+    """-> list of functions: (name, [Ins], {label: index})"""
+    funcs = []
+    cur = None
+    in_asm = False
+    for i, line in enumerate(lines):
+        s = line.split(";", 1)[0].strip() if not line.strip().startswith(";;#ASM") else line.strip()
+        if re.match(r"^_Z\S+:", s):
+            cur = (s.split(":")[0], [], {})
+            funcs.append(cur)
+            continue
+        if line.strip().startswith(";;#ASMSTART"):
+            in_asm = True
+            continue
+        if line.strip().startswith(";;#ASMEND"):
+            in_asm = False
+            continue
+        if cur is None or not s or s.startswith("."):
+            if cur is not None and re.match(r"^\.LBB\S+:", s):
+                cur[2][s.split(":")[0]] = len(cur[1])
+            continue
+        if s.endswith(":"):
+            cur[2][s[:-1]] = len(cur[1])
+            continue
+        cur[1].append(Ins(i + 1, s, in_asm))
+    return funcs
+
+
+def successors(ins, k, labels, n):
+    op = ins[k].op
+    if op == "s_endpgm" or op.startswith("s_setpc"):
+        return []
+    if op == "s_branch":
+        t = labels.get(ins[k].ops[0]) if ins[k].ops else None
+        return [t] if t is not None else []
+    if op.startswith("s_cbranch"):
+        t = labels.get(ins[k].ops[0]) if ins[k].ops else None
+        return [k + 1] + ([t] if t is not None else [])
+    return [k + 1] if k + 1 < n else []
+
+
+def walk_mfma(ins, labels, m, report):
+    mf = ins[m]
+    d, a, b, c = (rng(o.split()[0]) for o in (mf.ops + ["", "", "", ""])[:4])
+    src_c = regs(mf.ops[3].split()[0]) if len(mf.ops) > 3 else set()
+    src_c -= mf.dst  # srcC == dst (accumulate in place): nothing else may write it anyway
+    window = PASSES.get(mf.op, DEFAULT_PASSES)
+    n = len(ins)
+    seen = set()
+    stack = [(k, 0, frozenset(mf.dst), 0) for k in successors(ins, m, labels, n)]
+    while stack:
+        k, ws, pend, depth = stack.pop()
+        if k is None or k >= n or depth > 400:
+            continue
+        key = (k, min(ws, window), pend)
+        if key in seen:
+            continue
+        seen.add(key)
+        it = ins[k]
+        if it.asm and ws < window and it.dst & src_c:
+            report(it, f"asm write into srcC of the MFMA at line {mf.line} after {ws} wait state(s) (WAR, window {window})")
+        pend = pend - it.src
+        if it.dst & pend:
+            if it.asm:
+                report(it, f"asm write into pending dst of the MFMA at line {mf.line}")
+            pend = pend - it.dst
+        ws2 = ws + it.wait_states()
+        if ws2 >= window and not pend:
+            continue
+        for s in successors(ins, k, labels, n):
+            stack.append((s, ws2, pend, depth + 1))
+
+
+def lint(path, out=sys.stdout):
+    lines = open(path).read().split("\n")
+    funcs = parse(lines)
+    found = {}
+
+    for name, ins, labels in funcs:
+        for m, it in enumerate(ins):
+            if not it.op.startswith("v_mfma"):
+                continue
+            ops = [o.split()[0] for o in it.ops[:4]]
+            d, a, b, c = (rng(o) for o in ops)
+            why = []
+            if ov(d, c) and d != c:
+                why.append("partial dst/srcC overlap")
+            if (ov(d, a) and d != a) or (ov(d, b) and d != b):
+                why.append("dst partially over srcA/srcB")
+            if why:
+                found.setdefault((it.line, ", ".join(why)), (it, name))
+
+            def report(x, why, name=name):
+                found.setdefault((x.line, why), (x, name))
+
+            walk_mfma(ins, labels, m, report)
+    for (line, why), (x, name) in sorted(found.items()):
+        print(f"{line}: {x.text}    <- {why}  [{name[:60]}]", file=out)
+    print(f"{len(found)} suspect MFMA pattern(s)", file=out)
+    return found
+
+
+if __name__ == "__main__":
+    lint(sys.argv[1])
