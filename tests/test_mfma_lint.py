@@ -4,7 +4,9 @@ tools/mfma_lint.py follows every MFMA along all control-flow paths and flags inl
 instructions that (a) write a register of the MFMA's destination before anything has read it
 (WAW: the MFMA's write-back can land after the asm result; round 2 hit this in layer 3), or
 (b) write a register the MFMA reads as srcC within its pass window (WAR: a multi-pass MFMA reads
-srcC late).  The compiler's hazard checks do not cover inline asm.  The build must show neither.
+srcC late), (c) read the MFMA's result before its latency has passed, or (d) write a register a
+following MFMA reads fewer than 2 wait states later.  The compiler's hazard checks do not cover
+inline asm.  The build must show none of them.
 """
 import os
 import subprocess
@@ -52,6 +54,17 @@ _Z3bazPi:
 	v_ashr_pk_i8_i32 v40, v20, v21, 0
 	;;#ASMEND
 	s_endpgm
+_Z3quxPi:
+	v_mfma_i32_16x16x64_i8 v[0:3], v[4:7], v[12:15], v[8:11]
+	s_nop 3
+	;;#ASMSTART
+	v_ashr_pk_i8_i32 v30, v0, v1, 0
+	;;#ASMEND
+	;;#ASMSTART
+	v_ashr_pk_i8_i32 v13, v20, v21, 0
+	;;#ASMEND
+	v_mfma_i32_16x16x64_i8 v[40:43], v[4:7], v[12:15], 0
+	s_endpgm
 """
 
 
@@ -60,12 +73,18 @@ def test_lint_finds_hazards_across_branches(tmp_path):
     p.write_text(SYNTHETIC)
     with open(os.devnull, "w") as null:
         found = mfma_lint.lint(str(p), out=null)
-    whys = {line: why for (line, why) in found}
-    assert "WAR" in whys[8]            # fall-through after a conditional branch
-    assert "WAR" in whys[14]           # across a loop back edge (write at the loop head)
-    assert "pending dst" in whys[31]   # on the taken side of s_cbranch_execz
-    assert 24 not in whys and 23 not in whys             # 5 wait states after a 4-pass MFMA: outside the window
-    assert len(found) == 3
+    whys = {}
+    for (line, why) in found:
+        whys.setdefault(line, []).append(why)
+    has = lambda line, tag: any(tag in w for w in whys.get(line, []))  # noqa: E731
+    assert has(8, "WAR")               # fall-through after a conditional branch
+    assert has(14, "WAR")              # across a loop back edge (write at the loop head)
+    assert has(14, "RAW, needs 2")     # ... which is also read 1 wait state later by the MFMA
+    assert has(31, "pending dst")      # on the taken side of s_cbranch_execz
+    assert 24 not in whys and 23 not in whys             # 5 wait states after a 4-pass MFMA: outside the WAR window
+    assert has(38, "RAW, window 8")    # asm reads a 4-pass MFMA's result 4 states after it
+    assert has(41, "RAW, needs 2")     # MFMA reads an asm output with no wait state between
+    assert len(found) == 6
 
 
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")

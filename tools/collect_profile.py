@@ -2,8 +2,8 @@
 """Turns a tools/profile_round.sh output directory into the committed profile artefacts:
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
-  profiles/<tag>_pmc.csv            per-dispatch FETCH_SIZE / WRITE_SIZE of the forward kernel
-  profiles/pmc_traffic.json         HBM bytes per launch (read by bench.py for roofline.traffic)
+  profiles/<tag>_pmc_<cfg>.csv      per-dispatch WRITE_SIZE / TCC_EA0_RDREQ_* (configs B, C, D)
+  profiles/pmc_traffic.json         HBM bytes per launch per config (bench.py's roofline.traffic)
   profiles/<tag>_bench_*.json       the bench JSON lines
 
 FETCH_SIZE is doubled (gfx950 tallies 128-B fabric reads at 64 B: MI355X_MICROARCH.md, HBM
@@ -43,56 +43,61 @@ def main():
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(one(f"{src}/trace/**/*kernel_stats.csv"), f"{prof}/{tag}_kernel_stats.csv")
-    for cfg in ("b22", "c64", "d22"):
+    for cfg in ("b22", "c64", "d22", "p64"):
         p = f"{src}/bench_{cfg}.json"
         if os.path.exists(p):
             lines = [l for l in open(p) if l.startswith("{")]
             if lines:
                 open(f"{prof}/{tag}_bench_{cfg}.json", "w").write(lines[-1])
     fetch = pmc_values(one(f"{src}/pmc_fetch/**/*counter_collection.csv"), "FETCH_SIZE")
-    write = pmc_values(one(f"{src}/pmc_write/**/*counter_collection.csv"), "WRITE_SIZE")
-    rqf = glob.glob(f"{src}/pmc_rdreq/**/*counter_collection.csv", recursive=True)
     rcols = ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
-    rvals = {c: pmc_values(rqf[0], c) for c in rcols} if rqf else {c: [] for c in rcols}
-    with open(f"{prof}/{tag}_pmc.csv", "w") as f:
-        f.write("dispatch,FETCH_SIZE_kB,WRITE_SIZE_kB," + ",".join(rcols) + "\n")
-        for i in range(max(len(fetch), len(write), *(len(v) for v in rvals.values()))):
-            row = [fetch[i] if i < len(fetch) else "", write[i] if i < len(write) else ""]
-            row += [rvals[c][i] if i < len(rvals[c]) else "" for c in rcols]
-            f.write(f"{i}," + ",".join(str(x) for x in row) + "\n")
     # skip the first (warm-up) dispatch
     med = lambda v: sorted(v[1:] or v)[len(v[1:] or v) // 2]  # noqa: E731
-    fk = med(fetch)
-    wk = med(write)
-    write_bytes = wk * 1024
-    tj = {"config": "b22", "batch": 65536, "kernel": "k_forward<Cfg<22,1125,RB=1,CB=0>>",
-          "fetch_size_kB_raw": fk, "write_size_kB": wk, "write_bytes": write_bytes,
-          "alg_bytes_per_launch": (22 * 1125 + 4) * 65536}
-    rq = glob.glob(f"{src}/pmc_rdreq/**/*counter_collection.csv", recursive=True)
-    if rq:
-        # memory-side read requests by size: bytes = 32 n32 + 64 n64 + 128 n128 (the requests of
-        # other sizes, if any, are reported as the remainder and not counted)
-        n = {c: med(pmc_values(rq[0], c)) for c in ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum",
-                                                     "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")}
-        read_bytes = 32 * n["TCC_EA0_RDREQ_32B_sum"] + 64 * n["TCC_EA0_RDREQ_64B_sum"] + 128 * n["TCC_EA0_RDREQ_128B_sum"]
-        tj.update({"rdreq": n, "rdreq_other": n["TCC_EA0_RDREQ_sum"] - n["TCC_EA0_RDREQ_32B_sum"]
-                   - n["TCC_EA0_RDREQ_64B_sum"] - n["TCC_EA0_RDREQ_128B_sum"],
-                   "read_bytes": read_bytes, "read_bytes_fetch_size_x2": 2 * fk * 1024,
-                   "source": f"profiles/{tag}_pmc.csv (medians over dispatches after the first); reads from "
-                             "TCC_EA0_RDREQ_{32B,64B,128B}_sum (bytes by request size), writes WRITE_SIZE"})
-    else:
-        read_bytes = 2 * fk * 1024
-        tj.update({"read_bytes": read_bytes,
-                   "source": f"profiles/{tag}_pmc.csv (median over dispatches after the first; FETCH_SIZE x2 per gfx950 correction)"})
-    tj["hbm_bytes_per_launch"] = read_bytes + write_bytes
+    alg = {"b22": 22 * 1125 + 4, "c64": 64 * 1000 + 4, "d22": 22 * 1125 + 4}
+    kern = {"b22": (22, 1125), "c64": (64, 1000), "d22": (22, 1125)}
+    configs = {}
+    for cfg in ("b22", "c64", "d22"):
+        wf = glob.glob(f"{src}/pmc_write_{cfg}/**/*counter_collection.csv", recursive=True)
+        rq = glob.glob(f"{src}/pmc_rdreq_{cfg}/**/*counter_collection.csv", recursive=True)
+        if not (wf and rq):
+            continue
+        write = pmc_values(wf[0], "WRITE_SIZE")
+        rvals = {c: pmc_values(rq[0], c) for c in rcols}
+        with open(f"{prof}/{tag}_pmc_{cfg}.csv", "w") as f:
+            cols = ["WRITE_SIZE_kB", *rcols] + (["FETCH_SIZE_kB"] if cfg == "b22" else [])
+            f.write("dispatch," + ",".join(cols) + "\n")
+            series = [write, *(rvals[c] for c in rcols)] + ([fetch] if cfg == "b22" else [])
+            for i in range(max(len(v) for v in series)):
+                f.write(f"{i}," + ",".join(str(v[i]) if i < len(v) else "" for v in series) + "\n")
+        n = {c: med(rvals[c]) for c in rcols}
+        # memory-side read requests by size: bytes = 32 n32 + 64 n64 + 128 n128 (requests of other
+        # sizes, if any, are reported as the remainder and not counted); writes WRITE_SIZE (kB)
+        read_bytes = 32 * n[rcols[1]] + 64 * n[rcols[2]] + 128 * n[rcols[3]]
+        write_bytes = med(write) * 1024
+        tc = {"batch": 65536, "kernel": "k_forward<Cfg<%d,%d,RB=1,CB=0>>" % kern[cfg],
+              "rdreq": n, "rdreq_other": n[rcols[0]] - n[rcols[1]] - n[rcols[2]] - n[rcols[3]],
+              "read_bytes": read_bytes, "write_bytes": write_bytes,
+              "alg_bytes_per_launch": alg[cfg] * 65536,
+              "hbm_bytes_per_launch": read_bytes + write_bytes,
+              "ratio_to_algorithmic": (read_bytes + write_bytes) / (alg[cfg] * 65536),
+              "dispatches": len(rvals[rcols[0]])}
+        if cfg == "b22":
+            tc["fetch_size_kB_raw"] = med(fetch)
+            tc["read_bytes_fetch_size_x2"] = 2 * med(fetch) * 1024
+        configs[cfg] = tc
+    tj = {"source": f"profiles/{tag}_pmc_<config>.csv: medians over the dispatches after the first of one "
+                    "rocprofv3 --pmc pass per counter group and config (bench.py --steps 5 --warmup 1); reads "
+                    "from TCC_EA0_RDREQ_{32B,64B,128B}_sum (bytes by request size), writes WRITE_SIZE",
+          "configs": configs}
     json.dump(tj, open(f"{prof}/pmc_traffic.json", "w"), indent=1)
-    # the config-B bench line of this round carries this round's traffic (bench.py read the
-    # previous pmc_traffic.json when it ran, before these counter passes)
-    bp = f"{prof}/{tag}_bench_b22.json"
-    if os.path.exists(bp):
-        bl = json.loads(open(bp).read())
-        bl["roofline"]["traffic"] = tj["hbm_bytes_per_launch"]
-        open(bp, "w").write(json.dumps(bl) + "\n")
+    # this round's bench lines carry this round's traffic (bench.py read the previous
+    # pmc_traffic.json when it ran, before these counter passes)
+    for cfg, tc in configs.items():
+        bp = f"{prof}/{tag}_bench_{cfg}.json"
+        if os.path.exists(bp):
+            bl = json.loads(open(bp).read())
+            bl["roofline"]["traffic"] = tc["hbm_bytes_per_launch"]
+            open(bp, "w").write(json.dumps(bl) + "\n")
     # agreement check: rocprofv3 kernel-trace durations of the timed dispatches vs the HIP-event
     # average bench.py measured in the same (profiled) process
     trace = one(f"{src}/trace/**/*kernel_trace.csv")
@@ -103,7 +108,7 @@ def main():
     steps, warm = pb["steps"], pb["warmup"]
     timed = durs[-steps:]  # the timed launches are the process's last `steps` dispatches (after settle + warmup)
     summary = {
-        "kernel": tj["kernel"],
+        "kernel": configs["b22"]["kernel"],
         "rocprof_dispatches": len(durs),
         "rocprof_avg_ms_timed_dispatches": sum(timed) / len(timed),
         "bench_hip_event_avg_ms_same_process": pb["roofline"]["avg_kernel_ms"],

@@ -9,9 +9,16 @@
                              round-2 layer-3 fault)
   asm write into srcC (WAR)  an inline-asm instruction writes a register that an MFMA issued fewer
                              than W wait states earlier reads as srcC.  A multi-pass MFMA reads
-                             srcC late, so the write can reach the accumulator's C-init (the
-                             round-1 layer-1 fault).  srcA/srcB are read at issue
-                             and have no such window.
+                             srcC late, so the write could reach the accumulator's C-init (the
+                             round-2 verdict's hypothesis for the round-1 layer-1 fault; DESIGN.md
+                             §3 has what the lint found).  srcA/srcB are read at issue and have no
+                             such window.
+  asm read of MFMA result    an inline-asm instruction reads a register of an MFMA's destination
+                             fewer than R wait states after the MFMA (RAW: the result is not there
+                             yet; the compiler pads only for readers it emitted itself)
+  MFMA read of asm output    an MFMA reads as srcA/srcB/srcC a register an inline-asm instruction
+                             wrote fewer than 2 wait states earlier (VALU write -> MFMA operand
+                             read needs 2; hipcc pads one state after ;;#ASMEND)
 
 Why inline asm: the compiler's hazard recognizer inserts the required wait states (s_nop) for every
 instruction it emitted itself, but it cannot see into inline asm, so neither the WAR nor the WAW
@@ -20,7 +27,10 @@ window is guarded there.
 Wait states W are the compiler's own (GCNHazardRecognizer, gfx940 family), confirmed on the
 ROCm 7.2 compiler by probes that overwrite srcC right after an MFMA (it inserts exactly 3 wait
 states for v_mfma_i32_16x16x64_i8): 4-pass XDL 3, 8-pass 7, 16-pass 15.  The tool uses the pass
-count itself (one more than the compiler) as the window.
+count itself (one more than the compiler) as the window.  The result-read window R is what the
+compiler leaves before its own VALU readers in this kernel: 8 states after a 4-pass MFMA, 12
+after an 8-pass one (s_nop 6 behind the second of a pair / s_nop 11 behind a 32x32x32 chain);
+16-pass: 20.
 
 Control flow: each MFMA is followed along every path of the function (fall-through, s_branch
 targets, both sides of s_cbranch_*), so a hazard across a loop back edge or a branch is seen.
@@ -40,6 +50,11 @@ PASSES = {
     "v_mfma_i32_32x32x16_i8": 8,
 }
 DEFAULT_PASSES = 16  # unknown shape: assume the longest
+
+
+def raw_window(passes):
+    """wait states between an MFMA and the first VALU read of its result (see the header)"""
+    return 4 + passes
 
 
 def rng(tok):
@@ -152,16 +167,34 @@ def walk_mfma(ins, labels, m, report):
         it = ins[k]
         if it.asm and ws < window and it.dst & src_c:
             report(it, f"asm write into srcC of the MFMA at line {mf.line} after {ws} wait state(s) (WAR, window {window})")
+        if it.asm and ws < raw_window(window) and it.src & pend:
+            report(it, f"asm read of the result of the MFMA at line {mf.line} after {ws} wait state(s) (RAW, window {raw_window(window)})")
         pend = pend - it.src
         if it.dst & pend:
             if it.asm:
                 report(it, f"asm write into pending dst of the MFMA at line {mf.line}")
             pend = pend - it.dst
         ws2 = ws + it.wait_states()
-        if ws2 >= window and not pend:
+        if ws2 >= raw_window(window) and not pend:
             continue
         for s in successors(ins, k, labels, n):
             stack.append((s, ws2, pend, depth + 1))
+
+
+def asm_before_mfma(ins, m, report):
+    """MFMA at m reads an operand an inline-asm instruction wrote fewer than 2 wait states before
+    (straight-line look-back within the basic block)"""
+    mf = ins[m]
+    ws = 0
+    for k in range(m - 1, max(-1, m - 8), -1):
+        it = ins[k]
+        if it.op.startswith(("s_branch", "s_cbranch", "s_endpgm", "s_setpc")):
+            return
+        if it.asm and ws < 2 and it.dst & mf.src:
+            report(it, f"MFMA at line {mf.line} reads this asm output after {ws} wait state(s) (RAW, needs 2)")
+        ws += it.wait_states()
+        if ws >= 2:
+            return
 
 
 def lint(path, out=sys.stdout):
@@ -187,6 +220,7 @@ def lint(path, out=sys.stdout):
                 found.setdefault((x.line, why), (x, name))
 
             walk_mfma(ins, labels, m, report)
+            asm_before_mfma(ins, m, report)
     for (line, why), (x, name) in sorted(found.items()):
         print(f"{line}: {x.text}    <- {why}  [{name[:60]}]", file=out)
     print(f"{len(found)} suspect MFMA pattern(s)", file=out)
