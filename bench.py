@@ -129,11 +129,23 @@ def cpu_baseline(ps, x_dev, seconds):
     t1 = time.perf_counter()
     co.batch(s1, nthreads=1)
     d1 = time.perf_counter() - t1
+    # (ii') when a quota caps the thread count: also one thread per CPU of the whole affinity
+    # mask, on a bounded sample (about a fifth of the budget at the quota-limited rate)
+    mask = None
+    if threads < ncpu and "MIB_CPU_THREADS" not in os.environ:
+        nm = int(min(x_dev.shape[0], max(4 * ncpu, seconds / 5 / per_trial)))
+        sm = x_dev[:nm].cpu().numpy()
+        tm = time.perf_counter()
+        co.batch(sm, nthreads=ncpu)
+        dm = time.perf_counter() - tm
+        mask = {"value": nm / dm, "unit": "trials/s", "threads": ncpu,
+                "sample": f"{nm} trials, {ncpu} threads under a {quota}-CPU quota, {dm:.1f} s"}
     return {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
             "sample": f"{n} trials ({reps} pass(es) over the first {n // reps} trials) of the same synthetic batch, C restatement (oracle/oracle.c, -O3) "
                       f"of net_model_compute, {threads} host threads (one per usable CPU: affinity mask "
                       f"{ncpu}, cgroup quota {quota}) on {cpu}, {dt:.1f} s",
             "one_core": {"value": n1 / d1, "unit": "trials/s", "sample": f"{n1} trials, 1 thread, {d1:.1f} s"},
+            "affinity_mask_threads": mask,
             "host_cpus": {"affinity": ncpu, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota,
                           "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}}
 
