@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=65536, help="trials per GPU")
     ap.add_argument("--config", default="b22", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--variant", default="canonical", choices=("canonical", "plain_bn", "clip_balanced"),
+                    help="build variant the parameter blob selects: the canonical -DREORDER_BN build, the "
+                         "plain-BN branches (layer2.c:139-210, layer4.c:91-133) or golden-model balanced clipping")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed launches before the warmup steps (GPU clock ramp)")
@@ -188,7 +191,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group(backend, init_method="env://")
 
-    ps = ParamSet.synthetic(seed=a.seed, C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"])
+    ps = ParamSet.synthetic(seed=a.seed, C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"],
+                            reorder_bn=a.variant != "plain_bn", clip_balanced=a.variant == "clip_balanced")
     lib.params_load(ps)
     stride = lib.trial_stride()
     B = a.batch
@@ -265,13 +269,14 @@ def main():
             # (tools/collect_profile.py), per config under "configs"
             tj = json.load(open(a.traffic_json))
             tc = tj.get("configs", {}).get(a.config, tj if tj.get("config") == a.config else {})
-            if tc.get("batch") == B:
+            if tc.get("batch") == B and a.variant == "canonical":
                 traffic = tc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
         value = world * B * a.steps / elapsed
         out = {
-            "metric": METRIC if a.config == "b22" else f"EEG trials/sec ({cfg['name']}) at batch {B}",
+            "metric": (METRIC if a.config == "b22" and a.variant == "canonical"
+                       else f"EEG trials/sec ({cfg['name']}, {a.variant} build) at batch {B}"),
             "value": value,
             "unit": "trials/s",
             "n_gpus": world,
@@ -284,13 +289,14 @@ def main():
             "vs_baseline": None,
             "dtype": "int8",
             "data": "synthetic (uniform int8 EEG generated on device; seeded synthetic integer weights)",
-            "config": {"workload": cfg["name"], "C": cfg["C"], "T": cfg["T"], "batch_per_gpu": B,
+            "config": {"workload": cfg["name"], "variant": a.variant, "C": cfg["C"], "T": cfg["T"], "batch_per_gpu": B,
                        "global_batch": world * B, "weight_bits": cfg["wbits"],
                        "parallelism": f"dp{world} static batch split, no collectives",
                        "grid": info["grid"], "threads": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_forward<Cfg<%d,%d,RB=1,CB=0>>" % (cfg["C"], cfg["T"]),
+                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d>>" % (cfg["C"], cfg["T"], a.variant != "plain_bn",
+                                                                          a.variant == "clip_balanced"),
                          "avg_kernel_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes_trial * B},
             "cpu_baseline": None,
