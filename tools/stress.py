@@ -3,10 +3,13 @@
 outputs that differ from the expected ones.
 
   1. net_layer1 (k_layer stage 1) on the stress fixture, N1 calls, against the fixture's y1;
-  2. the fused batch kernel on B trials, N2 launches, each output compared with the oracle's
-     logits (computed once on the CPU for the same inputs).
+  2. the fused batch kernel on B trials, N2 launches per parameter mode.  The inputs are NB
+     distinct seeded batches (the oracle's logits computed once per batch on the CPU); launch i
+     runs batch i % NB under a fresh random trial permutation (drawn on the device), so every
+     launch maps different trials to different workgroups and prefetch slots, and is compared
+     with the oracle's logits permuted the same way.
 
-    python tools/stress.py [--lib path] [--n1 2000] [--n2 200] [--B 65536]
+    python tools/stress.py [--lib path] [--n1 2000] [--n2 200] [--nb 8] [--B 65536]
 """
 import argparse
 import os
@@ -29,6 +32,7 @@ def main():
     ap.add_argument("--n1", type=int, default=2000)
     ap.add_argument("--n2", type=int, default=200)
     ap.add_argument("--B", type=int, default=65536)
+    ap.add_argument("--nb", type=int, default=8, help="distinct input batches per parameter mode")
     a = ap.parse_args()
     if a.lib:
         lib.load(os.path.abspath(a.lib))
@@ -52,26 +56,36 @@ def main():
         ps = ParamSet.synthetic(seed=7, stress=stress)
         lib.params_load(ps)
         stride = lib.trial_stride()
-        g = torch.Generator(device="cuda:0").manual_seed(11)
-        x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0", generator=g)
-        x[:, 22 * 1125:] = 0
-        want = oracle.COracle(ps).batch(x.cpu().numpy(), nthreads=min(16, os.cpu_count() or 1))
-        want_t = torch.from_numpy(want).to("cuda:0")
+        g = torch.Generator(device="cuda:0").manual_seed(11 + stress)
+        xs, wants = [], []
+        t0 = time.time()
+        for k in range(a.nb):
+            x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0", generator=g)
+            x[:, 22 * 1125:] = 0
+            xs.append(x)
+            want = oracle.COracle(ps).batch(x.cpu().numpy(), nthreads=min(16, os.cpu_count() or 1))
+            wants.append(torch.from_numpy(want).to("cuda:0"))
+        print(f"oracle on {a.nb} x {a.B} trials: {time.time() - t0:.1f} s", flush=True)
+        xp = torch.empty_like(xs[0])
         y = torch.empty((a.B, 4), dtype=torch.int8, device="cuda:0")
         bad2 = 0
         t0 = time.time()
         for i in range(a.n2):
+            k = i % a.nb
+            perm = torch.randperm(a.B, device="cuda:0", generator=g)
+            torch.index_select(xs[k], 0, perm, out=xp)
             y.fill_(0x55)
-            lib.model_compute_batch(x.data_ptr(), y.data_ptr(), a.B)
+            lib.model_compute_batch(xp.data_ptr(), y.data_ptr(), a.B)
             torch.cuda.synchronize()
-            nb = int((y != want_t).any(dim=1).sum())
+            bad = (y != wants[k][perm]).any(dim=1)
+            nb = int(bad.sum())
             if nb:
                 bad2 += 1
                 if bad2 <= 5:
-                    rows = torch.nonzero((y != want_t).any(dim=1)).flatten()[:4].tolist()
+                    rows = torch.nonzero(bad).flatten()[:4].tolist()
                     print(f"batch launch {i}: {nb} trials differ, first {rows}", flush=True)
-        print(f"batch (stress={stress}): {bad2} of {a.n2} launches wrong ({time.time() - t0:.1f} s)", flush=True)
-
+        print(f"batch (stress={stress}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
+              f"{a.nb * a.B} distinct ({time.time() - t0:.1f} s)", flush=True)
 
 if __name__ == "__main__":
     main()
