@@ -687,7 +687,12 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
   const v4i magic = {FMAGIC_I, FMAGIC_I, FMAGIC_I, FMAGIC_I};
   const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(R.a31, *(const v4i*)(y2w + T.l3b), magic, 0, 0, 0);
   v4i acc2 = magic, b2 = magic;
-  if constexpr (K::L3RC > 0) {
+#ifdef MIB_DIAG_NOL3T2
+  constexpr bool T2 = false;  // diagnostic (timing proxy): no tile 2
+#else
+  constexpr bool T2 = K::L3RC > 0;
+#endif
+  if constexpr (T2) {
     const int* p = (const int*)(y2w + T.l3b2);  // 4-byte aligned
     b2 = (v4i){p[0], p[1], p[2], p[3]};
     acc2 = __builtin_amdgcn_mfma_i32_16x16x64_i8(R.a32, b2, magic, 0, 0, 0);
@@ -706,7 +711,7 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
     *(unsigned short*)dst = (unsigned short)pr;
     *(unsigned short*)(dst + K::Y3S) = (unsigned short)(pr >> 16);
   }
-  if constexpr (K::L3RC > 0) {
+  if constexpr (T2) {
     const int y = min(max((int)__builtin_fmaf(__int_as_float(acc2[0]), r3, c3), K::LO), 127);
     if (T.l3w2 >= 0) smem_y3[T.l3w2 + FPW * wave] = (int8_t)y;
   }
@@ -819,7 +824,8 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
 // insight): MIB_DIAG_NOBAR drops the in-loop barriers, MIB_DIAG_SAME_TRIAL makes every trial read
 // trial 0 (L2-resident), MIB_DIAG_NOL1RQ / NOPOOL / NOTAIL / NOL2 / NOL3 / NOL45 skip the
 // layer-1 requant, the layer-2 pooling, the layer-2 tail tile, layer 2, layer 3, layers 4-5;
-// MIB_DIAG_NOL1MFMA / NOL2MFMA replace the layer-1 / layer-2 full-tile MFMAs by a vector add.
+// MIB_DIAG_NOL1MFMA / NOL2MFMA replace the layer-1 / layer-2 full-tile MFMAs by a vector add;
+// MIB_DIAG_NOL3T2 drops layer 3's tile 2 (outputs past 128).
 #ifdef MIB_DIAG_NOBAR
 #define MIB_LOOP_BARRIER() ((void)0)
 #else
