@@ -21,6 +21,12 @@ extern "C" {
  * float reciprocal is exact over that range. */
 int mibminet_test_reciprocal(int32_t fac, int64_t vmax, int32_t kmax, int32_t magic, float* r, float* c);
 
+/* The floor-form constants of the plain-BN branches (layer2.c:139-210, layer4.c:113-130: every
+ * element requantised, then the ReLU): for |x| <= vmax, e = clamp(floor(x / fac), 0, emax) is
+ * computed as bits(fmed3(fma(f32 bits (mbits + x), r, c), K, K + emax)) - bits(K), K = 1.5 * 2^23.
+ * Returns 0 with mbits (the magic the MFMA C-init adds to the offset), r and c, or NET_ERR_RANGE. */
+int mibminet_test_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* mbits, float* r, float* c);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,6 +21,7 @@ constexpr int L2_TAPS = 64;
 constexpr int L3_TAPS = 16;
 constexpr int ND5_MAX = 96;     // dwords of the layer-4 output [F2][T64_ALIGN] (F2*T64_ALIGN <= 384)
 constexpr int FMAGIC_I = 0x4B400000;   // bit pattern of 1.5 * 2^23
+constexpr float FMAGIC_F = 12582912.0f; // 1.5 * 2^23
 // REORDER_BN pooling bias: the layer-2 MFMA chains start from a bias B (the bits of a
 // float MFMA srcC inline constant), so every conv value a lies at a + B with no wrap (|a| < 2^22),
 // and max(a, thr) - thr = sat_u32((a + B) - (thr + B)): one full-rate v_sub_u32 clamp per element
@@ -63,8 +64,9 @@ struct SmallParams {
   int l4_thr[F2];         // -(net_l4_offset >> 3)
   int l4_offm[F2];        // net_l4_offset + 8 thr
   float l4_r[F2];
-  // plain (non-REORDER_BN) layer-2/4 branches: per-element BN with offset >> 3 and factor >> 3,
-  // as magic-offset MFMA C-init (offset + FMAGIC_I), reciprocal and -(1.5 * 2^23) * r
+  // plain (non-REORDER_BN) layer-2/4 branches: per-element BN with offset >> 3 and factor >> 3 in
+  // the floor form (mibminet.hip, choose_floor_form): MFMA C-init = per-filter magic bits + offset,
+  // reciprocal r and integer-valued c, so that fma(acc bits, r, c) = FMAGIC + floor(element)
   int l2n_ci[F2];
   float l2n_r[F2];
   float l2n_c[F2];

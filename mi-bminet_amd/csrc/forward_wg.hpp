@@ -491,24 +491,35 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
 
 // ---- layer 2 ---------------------------------------------------------------------------------
 // Plain (non-REORDER_BN) branch, layer2.c:139-210: each element requantised and clipped
-// (func_xcorr_scale -> transform.c:224), ReLU, sum of 8, >> 3.  acc holds the elements as
-// float bits (C-init = offset + FMAGIC_I), so q = fma(bits, r, c) = RN((x + off) * r);
-// med3(trunc(q), 0, 127) is clip-then-ReLU in one instruction.
-__device__ __forceinline__ unsigned l2n_out(const v16i& acc, float r, float c) {
-  int s[2];
+// (func_xcorr_scale -> transform.c:224), ReLU, sum of 8, >> 3.  Behind the ReLU, trunc equals
+// floor, so each element is the floor form of mibminet.hip (choose_floor_form): acc holds the float
+// bits of M + x (C-init = per-filter magic + offset) and fma(bits, r, c) = FMAGIC + floor(x / f) on
+// every reachable x (host-verified); fmed3 to [FMAGIC, FMAGIC + 127] is the clip and the ReLU, and
+// the bits of FMAGIC + e are FMAGIC_I + e, so a window's sum is its bits' integer sum minus
+// 8 FMAGIC_I (mod 2^32).  No float->int convert per element.
+template <int EMAX>
+__device__ __forceinline__ f2 floor_form2(int a, int b, float r, float c) {
+  const f2 q = __builtin_elementwise_fma((f2){__int_as_float(a), __int_as_float(b)}, (f2){r, r}, (f2){c, c});
+  constexpr float HI = FMAGIC_F + (float)EMAX;
+  return (f2){__builtin_amdgcn_fmed3f(q[0], FMAGIC_F, HI), __builtin_amdgcn_fmed3f(q[1], FMAGIC_F, HI)};
+}
+
+// sum of the eight floor-form elements acc[BASE .. BASE + 7] (e in [0, EMAX] each)
+template <int BASE, int EMAX>
+__device__ __forceinline__ unsigned floor_sum8(const v16i& acc, float r, float c) {
+  unsigned e[8];
 #pragma unroll
-  for (int w = 0; w < 2; w++) {
-    int e[8];
-#pragma unroll
-    for (int i = 0; i < 8; i += 2) {
-      const f2 q = __builtin_elementwise_fma((f2){__int_as_float(acc[8 * w + i]), __int_as_float(acc[8 * w + i + 1])},
-                                             (f2){r, r}, (f2){c, c});
-      e[i] = (int)__builtin_amdgcn_fmed3f(q[0], 0.0f, 127.0f);  // trunc(clamp) == clamp(trunc)
-      e[i + 1] = (int)__builtin_amdgcn_fmed3f(q[1], 0.0f, 127.0f);
-    }
-    s[w] = ((e[0] + e[1] + e[2]) + (e[3] + e[4]) + (e[5] + e[6])) + e[7];
+  for (int i = 0; i < 8; i += 2) {
+    const f2 q = floor_form2<EMAX>(acc[BASE + i], acc[BASE + i + 1], r, c);
+    e[i] = (unsigned)__float_as_int(q[0]);
+    e[i + 1] = (unsigned)__float_as_int(q[1]);
   }
-  return (unsigned)(s[0] >> 3) | ((unsigned)(s[1] >> 3) << 8);
+  return ((e[0] + e[1] + e[2]) + (e[3] + e[4]) + (e[5] + e[6])) + (e[7] - 8u * (unsigned)FMAGIC_I);
+}
+
+__device__ __forceinline__ unsigned l2n_out(const v16i& acc, float r, float c) {
+  const unsigned s0 = floor_sum8<0, 127>(acc, r, c), s1 = floor_sum8<8, 127>(acc, r, c);
+  return (s0 >> 3) | ((s1 >> 3) << 8);
 }
 
 // Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].
@@ -558,11 +569,10 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
     const int thrb = tp[0];
     part = (int)((relu_b(tacc[0], thrb) + relu_b(tacc[1], thrb)) + (relu_b(tacc[2], thrb) + relu_b(tacc[3], thrb)));
   } else {
-    const float r = sp->l2n_r[fcol], c = sp->l2n_c[fcol];
-    const f2 q01 = __builtin_elementwise_fma((f2){__int_as_float(tacc[0]), __int_as_float(tacc[1])}, (f2){r, r}, (f2){c, c});
-    const f2 q23 = __builtin_elementwise_fma((f2){__int_as_float(tacc[2]), __int_as_float(tacc[3])}, (f2){r, r}, (f2){c, c});
-    part = ((int)__builtin_amdgcn_fmed3f(q01[0], 0.0f, 127.0f) + (int)__builtin_amdgcn_fmed3f(q01[1], 0.0f, 127.0f)) +
-           ((int)__builtin_amdgcn_fmed3f(q23[0], 0.0f, 127.0f) + (int)__builtin_amdgcn_fmed3f(q23[1], 0.0f, 127.0f));
+    const float r = sp->l2n_r[fcol], c = sp->l2n_c[fcol];  // floor form (l2n_out)
+    const f2 q01 = floor_form2<127>(tacc[0], tacc[1], r, c), q23 = floor_form2<127>(tacc[2], tacc[3], r, c);
+    part = (int)(((unsigned)__float_as_int(q01[0]) + (unsigned)__float_as_int(q01[1])) +
+                 ((unsigned)__float_as_int(q23[0]) + (unsigned)__float_as_int(q23[1])) - 4u * (unsigned)FMAGIC_I);
   }
   const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)part, (unsigned)part, false, false);
   const int tot = (int)sw[0] + (int)sw[1];  // whole window (rows 2k and 2k+1 hold the same)
@@ -737,22 +747,11 @@ __device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* s
     return sat8x2<K::LO>((int)q[0], (int)q[1]);
   } else {
     // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
-    // sum of 8, >> 3, clip.  Elements are clamped to [0, 1024]: any element >= 1024 already
-    // saturates the result, and the reciprocal is verified exact up to there.
+    // sum of 8, >> 3, clip.  Elements in the floor form (l2n_out), clamped to [0, 1024]: any
+    // element >= 1024 already saturates the result, and the host verified the form up to there.
     const float rn = MIB_K4(sp->l4n_r, float), cn = MIB_K4(sp->l4n_c, float);
-    int sm[2];
-#pragma unroll
-    for (int hw = 0; hw < 2; hw++) {
-      int e[8];
-#pragma unroll
-      for (int j = 0; j < 8; j += 2) {
-        const f2 q = __builtin_elementwise_fma((f2){__int_as_float(acc[8 * hw + j]), __int_as_float(acc[8 * hw + j + 1])},
-                                               (f2){rn, rn}, (f2){cn, cn});
-        e[j] = (int)__builtin_amdgcn_fmed3f(q[0], 0.0f, 1024.0f);
-        e[j + 1] = (int)__builtin_amdgcn_fmed3f(q[1], 0.0f, 1024.0f);
-      }
-      sm[hw] = min((((e[0] + e[1] + e[2]) + (e[3] + e[4]) + (e[5] + e[6])) + e[7]) >> 3, 127);
-    }
+    const int sm[2] = {min((int)(floor_sum8<0, 1024>(acc, rn, cn) >> 3), 127),
+                       min((int)(floor_sum8<8, 1024>(acc, rn, cn) >> 3), 127)};
     return (unsigned)sm[0] | ((unsigned)sm[1] << 8);
   }
 }

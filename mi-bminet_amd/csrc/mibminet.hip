@@ -116,6 +116,88 @@ bool choose_reciprocal(int32_t fac, float* out, float* magic_c = nullptr, int64_
   return false;
 }
 
+// ---- floor-form element requant (plain-BN branches) ----------------------------------------
+// The plain branches requantise every conv element and apply the ReLU right after:
+// e = max(clip(trunc(x / fac)), 0) (layer2.c:139-210, layer4.c:113-130).  Behind the ReLU, trunc and
+// floor agree (they differ only for negative quotients, which both clamp to 0), so
+// e = clamp(floor(x / fac), 0, emax).  The GPU computes it without a float->int convert:
+//   g(x) = fma(bits_as_float(Mbits + x), r, c)        (one rounding, round-to-nearest-even)
+//   e    = bits(fmed3(g, K, K + emax)) - bits(K),       K = 1.5 * 2^23 (FMAGIC)
+// The MFMA C-init carries Mbits + offset, so the accumulator's bits are exactly float(M + x).  The
+// exact value of the fma is K + delta + x r with delta = M r + c - K; c is an integer-valued float
+// that f32 holds exactly, so delta = M r - n for the integer n = K - c, and M is searched so that delta
+// sits just below -1/2: then RN(K + delta + x r) = K + floor(x / fac) at every step boundary.  g is
+// monotone in x, so checking both ends of every step interval k = -1 .. emax of the reachable range
+// |x| <= vmax (with std::fmaf, the same correctly rounded fma) proves it for every reachable x.
+float floor_form(int32_t mbits, int64_t x, float r, float c) {
+  float m;
+  const int32_t b = mbits + (int32_t)x;
+  std::memcpy(&m, &b, 4);
+  return std::fmaf(m, r, c);
+}
+
+bool verify_floor_form(int32_t fac, int32_t mbits, float r, float c, int64_t emax, int64_t vmax) {
+  const int64_t F = fac < 0 ? -(int64_t)fac : (int64_t)fac;
+  const float K = 12582912.0f;
+  for (int64_t k = -1; k <= emax; k++) {
+    // x with floor(x / fac) == k: fac > 0: [k F, k F + F - 1]; fac < 0: [-(k + 1) F + 1, -k F]
+    int64_t lo = fac > 0 ? k * F : -(k + 1) * F + 1;
+    int64_t hi = fac > 0 ? k * F + F - 1 : -k * F;
+    if (lo > vmax || hi < -vmax) continue;
+    lo = std::max(lo, -vmax);
+    hi = std::min(hi, vmax);
+    const int64_t want = std::min(std::max(k, (int64_t)0), emax);
+    for (const int64_t x : {lo, hi}) {
+      const float g = floor_form(mbits, x, r, c);
+      const double e = std::min(std::max((double)g, (double)K), (double)K + (double)emax) - (double)K;
+      if (e != (double)want) return false;
+    }
+  }
+  return true;
+}
+
+bool choose_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* mbits, float* r_out, float* c_out) {
+  if (fac == 0 || vmax >= (1 << 22) || emax > 1024) return false;
+  const double F = std::fabs((double)fac);
+  const double K = 12582912.0;
+  const int64_t mlo = (1 << 23) + vmax, mhi = (1 << 24) - 1 - vmax;  // M + x stays in [2^23, 2^24)
+  // target delta: -1/2 + 1/(2F), the middle of the window that maps each step to its floor
+  const double target = -0.5 + 0.5 / F;
+  float r = std::nextafterf(std::nextafterf((float)(1.0 / F), 0.0f), 0.0f);
+  for (int tries = 0; tries < 16; tries++, r = std::nextafterf(r, INFINITY)) {
+    const double rs = fac < 0 ? -(double)r : (double)r;
+    // for each integer n, M = round((n + target) / rs) puts delta = M rs - n within rs / 2 of the
+    // target; successive n give different residues, and the check below decides
+    const double t0 = std::min((double)mlo * rs, (double)mhi * rs);
+    const int64_t n0 = (int64_t)std::ceil(t0 - target) + 1;
+    for (int64_t i = 0; i < 512 + 128; i++) {
+      int64_t n, M;
+      if (i < 512) {
+        n = n0 + i;
+        M = std::llround(((double)n + target) / rs);
+      } else {
+        // |fac| so large that M r moves by less than 1 over the whole magic range (every reachable
+        // output is 0 or 1): the first magics with n on either side of M r
+        M = mlo + (i - 512) / 2;
+        n = (int64_t)((i & 1) ? std::ceil((double)M * rs) : std::floor((double)M * rs));
+      }
+      if (M < mlo || M > mhi) continue;
+      const double c = K - (double)n;  // integer-valued (exact in f32 below 2^24, and when even below 2^25)
+      if ((double)(float)c != c) continue;
+      const float Mf = (float)M;
+      int32_t mb;
+      std::memcpy(&mb, &Mf, 4);
+      if (verify_floor_form(fac, mb, (float)rs, (float)c, emax, vmax)) {
+        *mbits = mb;
+        *r_out = (float)rs;
+        *c_out = (float)c;
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
 // ---- blob parsing ------------------------------------------------------------------------
 struct Reader {
   const uint8_t* p;
@@ -220,18 +302,21 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
   }
   if (128LL + (int64_t)F2 * d.T64() * A >= (1 << 24)) return NET_ERR_RANGE;
   if (!hp.reorder_bn) {
-    // plain branches: per-element BN with offset >> 3 and factor >> 3 through the magic-offset
-    // C-init (|x + off| < 2^22); layer 4's elements are exact up to the 1024 clamp
+    // plain branches: per-element BN with offset >> 3 and factor >> 3, ReLU right after, in the
+    // floor form (choose_floor_form): the MFMA C-init is the per-filter magic plus the offset
+    // (|x| < 2^22), layer 2's elements clamp to [0, 127], layer 4's to [0, 1024] (anything above
+    // saturates the result)
     for (int f = 0; f < F2; f++) {
       const int32_t f2 = hp.l2_factor[f] >> 3, o2 = hp.l2_offset[f] >> 3;
       const int32_t f4 = hp.l4_factor[f] >> 3, o4 = hp.l4_offset[f] >> 3;
       if (f2 == 0 || f4 == 0) return NET_ERR_RANGE;
       const int64_t v2 = 64LL * A + std::llabs((int64_t)o2), v4 = (int64_t)F2 * A + std::llabs((int64_t)o4);
       if (v2 >= (1 << 22) || v4 >= (1 << 22)) return NET_ERR_RANGE;
-      dp.sp.l2n_ci[f] = o2 + FMAGIC_I;
-      dp.sp.l4n_ci[f] = o4 + FMAGIC_I;
-      if (!choose_reciprocal(f2, &dp.sp.l2n_r[f], &dp.sp.l2n_c[f], 128, v2)) return NET_ERR_RANGE;
-      if (!choose_reciprocal(f4, &dp.sp.l4n_r[f], &dp.sp.l4n_c[f], 1025, v4)) return NET_ERR_RANGE;
+      int32_t m2, m4;
+      if (!choose_floor_form(f2, 127, v2, &m2, &dp.sp.l2n_r[f], &dp.sp.l2n_c[f])) return NET_ERR_RANGE;
+      if (!choose_floor_form(f4, 1024, v4, &m4, &dp.sp.l4n_r[f], &dp.sp.l4n_c[f])) return NET_ERR_RANGE;
+      dp.sp.l2n_ci[f] = m2 + o2;
+      dp.sp.l4n_ci[f] = m4 + o4;
     }
   }
   // layer 1: B operand (column j of N-tile t: filter 8t + j/2, parity j&1 when P == 2)
@@ -745,6 +830,11 @@ int net_pack_trials_i8(const int8_t* x, int8_t* y, size_t B, int C, int T, int d
 int mibminet_test_reciprocal(int32_t fac, int64_t vmax, int32_t kmax, int32_t magic, float* r, float* c) {
   if (!r || (magic && !c) || vmax < 0 || vmax >= (1 << 24)) return NET_ERR_INVALID;
   return choose_reciprocal(fac, r, magic ? c : nullptr, kmax, vmax) ? NET_OK : NET_ERR_RANGE;
+}
+
+int mibminet_test_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* mbits, float* r, float* c) {
+  if (!mbits || !r || !c || vmax < 0 || emax < 0) return NET_ERR_INVALID;
+  return choose_floor_form(fac, emax, vmax, mbits, r, c) ? NET_OK : NET_ERR_RANGE;
 }
 
 int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int device, void* stream) {

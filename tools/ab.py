@@ -26,10 +26,12 @@ def main():
     ap.add_argument("--B", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variant", default="canonical", choices=("canonical", "plain_bn", "clip_balanced"))
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     C, T = {"b22": (22, 1125), "c64": (64, 1000)}[a.cfg]
-    blob = ParamSet.synthetic(seed=1, C=C, T=T).to_blob()
+    blob = ParamSet.synthetic(seed=1, C=C, T=T, reorder_bn=a.variant != "plain_bn",
+                              clip_balanced=a.variant == "clip_balanced").to_blob()
     libs = []
     for p in a.libs:
         L = ctypes.CDLL(os.path.abspath(p), mode=ctypes.RTLD_LOCAL)
