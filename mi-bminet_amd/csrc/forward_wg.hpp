@@ -432,6 +432,12 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
     const L1Tile& T = R.tile(t);
 #ifdef MIB_DIAG_NOL1MFMA
     accs[t] = a + T.wf;
+#elif defined(MIB_DIAG_L1K32)
+    {  // timing/energy proxy (results wrong): the same MFMA count at K = 32 (half the MAC slots)
+      typedef int v2i __attribute__((ext_vector_type(2)));
+      const long av = ((long)(unsigned)a[1] << 32) | (unsigned)a[0], bv = ((long)(unsigned)T.wf[1] << 32) | (unsigned)T.wf[0];
+      accs[t] = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv, (v4i){T.ci, T.ci, T.ci, T.ci}, 0, 0, 0);
+    }
 #else
     accs[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, T.wf, (v4i){T.ci, T.ci, T.ci, T.ci}, 0, 0, 0);
 #endif
@@ -824,7 +830,8 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
 // trial 0 (L2-resident), MIB_DIAG_NOL1RQ / NOPOOL / NOTAIL / NOL2 / NOL3 / NOL45 skip the
 // layer-1 requant, the layer-2 pooling, the layer-2 tail tile, layer 2, layer 3, layers 4-5;
 // MIB_DIAG_NOL1MFMA / NOL2MFMA replace the layer-1 / layer-2 full-tile MFMAs by a vector add;
-// MIB_DIAG_NOL3T2 drops layer 3's tile 2 (outputs past 128).
+// MIB_DIAG_NOL3T2 drops layer 3's tile 2 (outputs past 128); MIB_DIAG_L1K32 runs layer 1's MFMAs
+// at K = 32.
 #ifdef MIB_DIAG_NOBAR
 #define MIB_LOOP_BARRIER() ((void)0)
 #else
