@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--n2", type=int, default=200)
     ap.add_argument("--B", type=int, default=65536)
     ap.add_argument("--nb", type=int, default=8, help="distinct input batches per parameter mode")
+    ap.add_argument("--variants", default="canonical",
+                    help="comma list of build variants to stress: canonical, plain_bn, clip_balanced")
     a = ap.parse_args()
     if a.lib:
         lib.load(os.path.abspath(a.lib))
@@ -52,8 +54,10 @@ def main():
                 print(f"layer1 call {i}: {nb} bytes differ, first {w[:4].tolist()}", flush=True)
     print(f"layer1: {bad1} of {a.n1} calls wrong ({time.time() - t0:.1f} s)", flush=True)
 
-    for stress in (True, False):
-        ps = ParamSet.synthetic(seed=7, stress=stress)
+    modes = [(v, st) for v in a.variants.split(",") for st in (True, False)]
+    for variant, stress in modes:
+        ps = ParamSet.synthetic(seed=7, stress=stress, reorder_bn=variant != "plain_bn",
+                                clip_balanced=variant == "clip_balanced")
         lib.params_load(ps)
         stride = lib.trial_stride()
         g = torch.Generator(device="cuda:0").manual_seed(11 + stress)
@@ -84,7 +88,7 @@ def main():
                 if bad2 <= 5:
                     rows = torch.nonzero(bad).flatten()[:4].tolist()
                     print(f"batch launch {i}: {nb} trials differ, first {rows}", flush=True)
-        print(f"batch (stress={stress}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
+        print(f"batch ({variant}, stress={stress}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
               f"{a.nb * a.B} distinct ({time.time() - t0:.1f} s)", flush=True)
 
 if __name__ == "__main__":
