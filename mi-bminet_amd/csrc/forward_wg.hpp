@@ -7,27 +7,30 @@
 //           input window (P = 2 samples of C <= 32 channels per group, or 1 sample of up to 64)
 //           read straight from HBM into registers (4-byte-aligned 16-B loads, prefetched one
 //           trial ahead while the current trial runs layers 2-5); B = per-(filter, parity)
-//           weight fragment; C-init = offset + float magic, so requant is one exact packed fma,
-//           a truncating convert and a saturating pack (v_ashr_pk_i8_i32) per 2-4 samples.
+//           weight fragment; C-init = offset + float magic, so requant is one exact fma per
+//           output, a truncating convert and a saturating pack (v_ashr_pk_i8_i32) per 2 outputs.
 //                                                    (reference: layer1.c:53-101)
 //   layer2  64-tap depthwise temporal xcorr as a banded-Toeplitz GEMM on MFMA i32_32x32x32_i8:
 //           A = 32 output shifts x 96-tap band of the filter (held in registers; rows permuted so
 //           that each lane owns two whole pool-8 windows), B = 16-byte slices of the layer-1 row
-//           at immediate offsets.  32 column blocks per filter form its full tile.  The 32 TB
-//           outputs left per filter run on MFMA i32_16x16x64_i8 (16 shifts x 128-slot band, A
-//           from LDS): columns of 16 outputs, the wave's FPW filters side by side (block-diagonal
-//           K: each filter's MFMAs read the zero row for the other filter's columns); a lane
-//           holds half a pool window, the two halves meet by v_permlane16_swap.
-//                                                    (reference: layer2.c:56-118, xcorr.c:44)
-//   layer3  16-tap depthwise conv on MFMA i32_16x16x32_i8: A = 16 shifts x 32-byte band of the
-//           filter (registers), B = aligned 8-byte slices of the layer-2 row (columns = blocks of
-//           16 outputs); written transposed [u][f] (the reference's flip is index math).
+//           at immediate offsets.  32 column blocks per filter form its full tile; the chain starts
+//           from a float inline constant so the ReLU-pool is one saturating v_sub_u32 per element
+//           (biased pooling).  The TB blocks of 32 outputs left per filter (the tail) run on one
+//           3-step MFMA i32_16x16x64_i8 chain per wave (16 shifts, A from LDS): columns of 16
+//           outputs, the wave's two filters side by side with a block-diagonal K (a lane reads the
+//           zero chunk in the other filter's slots); a lane holds half a pool window, the two
+//           halves meet by v_permlane16_swap.    (reference: layer2.c:56-118, xcorr.c:44)
+//   layer3  16-tap depthwise conv on MFMA i32_16x16x64_i8, both filters of a wave in one tile
+//           (block-diagonal K): tile 1 = the first 128 outputs of each filter (16-output columns),
+//           tile 2 = the outputs past 128, four per column in register 0; C-init = float magic;
+//           written transposed [u][f] (the reference's flip is index math).
 //                                                    (reference: layer3.c:49-79, conv.c:105)
 //   layer4  16x16 pointwise on MFMA i32_32x32x32_i8 with a block-diagonal B (two 32-sample time
-//           blocks per MFMA, all 64 lanes busy) + ReLU + pool 8 + requant.
+//           blocks per MFMA, all 64 lanes busy) + biased ReLU pooling + requant.
 //                                                    (reference: layer4.c:51-149)
 //   layer5  F2*T64 -> 4 linear + bias + requant: one wave, 16 lanes per class, DPP row
 //           reduction, one dword store.              (reference: layer5.c:43-89)
+// The plain (non-REORDER_BN) build requantises every layer-2/4 element in the floor form (l2n_out).
 #pragma once
 #include "forward_common.hpp"
 
