@@ -695,6 +695,8 @@ int quantize_input(const F* x, int8_t* y, size_t B, int C, int T, F scale, int d
   if ((!x || !y) && B) return NET_ERR_INVALID;
   if (C < 1 || C > quant::CMAX || T < 1 || device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
   if (B > (size_t)INT32_MAX || !(scale > 0)) return NET_ERR_INVALID;
+  // one trial's input bytes form one buffer view (32-bit range); the tiles leave as 16-byte stores
+  if ((size_t)C * T * sizeof(F) >= (size_t)1 << 31 || ((uintptr_t)y & 15)) return NET_ERR_INVALID;
   if (B == 0) return NET_OK;
   if (const int rc = check_device(device)) return rc;
   const int stride = (int)(((size_t)C * T + 15) / 16 * 16);
@@ -713,6 +715,12 @@ int argmax_batch(const int8_t* logits, int32_t* out, size_t B, int N, int device
   if (const int rc = check_device(device)) return rc;
   DeviceGuard guard(device);
   if (guard.err != hipSuccess) return hip_err(guard.err);
+  if (N == 4 && ((uintptr_t)logits & 15) == 0 && ((uintptr_t)out & 15) == 0) {
+    const unsigned grid = (unsigned)((B + 4 * cls::CTHREADS - 1) / (4 * cls::CTHREADS));
+    hipLaunchKernelGGL(cls::k_argmax4, dim3(grid), dim3(cls::CTHREADS), 0, (hipStream_t)stream,
+                       (const unsigned*)logits, out, (int)B);
+    return hip_err(hipGetLastError());
+  }
   const unsigned grid = (unsigned)((B + cls::CTHREADS - 1) / cls::CTHREADS);
   hipLaunchKernelGGL(cls::k_argmax, dim3(grid), dim3(cls::CTHREADS), 0, (hipStream_t)stream, logits, out, (int)B, N);
   return hip_err(hipGetLastError());

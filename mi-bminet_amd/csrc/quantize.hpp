@@ -8,11 +8,15 @@
 //                                                           to nearest in that precision)
 // (* 254 then / 2 equals * 127 exactly: scaling by 2 commutes with rounding.)
 //
-// HBM-bound streaming transpose: one workgroup per (64-sample time tile, trial; batches past
-// 65,535 trials loop over trials in the workgroup); reads the
-// C rows of the tile coalesced along time, quantises, transposes through LDS and writes the
-// tile's 64 * C output bytes as contiguous dwords.  The trial's pad bytes (stride - C * T) are
-// written as zeros by the last tile.
+// HBM-bound streaming transpose.  One workgroup (4 waves) per (tile of TT = 256 time samples,
+// trial); batches past 65,535 trials loop over trials in the workgroup.  Each lane loads 4
+// consecutive samples of one channel row with one wide raw buffer load (float: 16 B, double:
+// 2 x 16 B, int8: 8 B at a 4-byte-aligned offset and a byte align), so a row's 256 samples are one
+// coalesced wave-instruction (two for double); the waves take rows w, w + 4, ... and issue the
+// loads of 4 rows before using any.  The buffer view of a trial ends at its own bytes (rounded up to
+// a dword), so loads past the last row's end read zeros instead of the next trial's samples.  Quantised bytes go into the
+// tile in LDS at [t][c]; the tile, which is contiguous in the output, then leaves as 16-byte
+// stores.  The last tile of a trial also writes the trial's pad bytes (stride - C T) as zeros.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -20,10 +24,12 @@
 namespace mib {
 namespace quant {
 
-constexpr int TT = 64;          // time samples per tile
-constexpr int QTHREADS = 256;
+constexpr int TT = 256;         // time samples per tile (4 per lane)
+constexpr int QTHREADS = 256;   // 4 waves
+constexpr int QWAVES = QTHREADS / 64;
 constexpr int CMAX = 64;
-constexpr int YMAX = 65535;   // grid.y limit: trials per launch row (larger batches loop)
+constexpr int YMAX = 65535;     // grid.y limit: trials per launch row (larger batches loop)
+constexpr int RCHUNK = 4;       // rows per wave whose loads are in flight together
 
 template <class F>
 __device__ __forceinline__ int quantize_one(F x, F s);
@@ -49,37 +55,93 @@ __device__ __forceinline__ int quantize_one<int8_t>(int8_t x, int8_t) {
   return x;
 }
 
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+
+// 4 consecutive samples of one row as raw bits, loaded from byte offset `off` of the trial's view
+template <class F>
+struct Row4;
+
+template <>
+struct Row4<float> {
+  v4u v;
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int off) {
+    v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  }
+  __device__ __forceinline__ float get(int j) const { return __uint_as_float(v[j]); }
+};
+
+template <>
+struct Row4<double> {
+  v4u lo, hi;
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int off) {
+    lo = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    hi = __builtin_amdgcn_raw_buffer_load_b128(r, off + 16, 0, 0);
+  }
+  __device__ __forceinline__ double get(int j) const {
+    const v4u& w = j < 2 ? lo : hi;
+    const int k = 2 * (j & 1);
+    return __hiloint2double((int)w[k + 1], (int)w[k]);
+  }
+};
+
+template <>
+struct Row4<int8_t> {
+  unsigned w;
+  __device__ __forceinline__ void load(__amdgpu_buffer_rsrc_t r, int off) {
+    // 8 bytes from the 4-byte-aligned offset below, then the 4 wanted bytes by a byte align
+    const v2u d = __builtin_amdgcn_raw_buffer_load_b64(r, off & ~3, 0, 0);
+    w = __builtin_amdgcn_alignbyte(d[1], d[0], (unsigned)(off & 3));
+  }
+  __device__ __forceinline__ int8_t get(int j) const { return (int8_t)(w >> (8 * j)); }
+};
+
 template <class F>
 __global__ __launch_bounds__(QTHREADS) void k_quantize(const F* __restrict__ x, int8_t* __restrict__ y,
                                                        int C, int T, int stride, F s, int B) {
-  __shared__ __attribute__((aligned(16))) int8_t tile[TT * CMAX];
+  __shared__ __attribute__((aligned(16))) int8_t tile[TT * CMAX + 16];
   const int t0 = blockIdx.x * TT;
   const int nt = min(TT, T - t0);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tl = 4 * lane;  // the lane's first sample in the tile
+  const bool last = t0 + TT >= T;
+  // bytes this tile writes: its nt * C samples, and for the last tile the pad up to the stride
+  const int nout = last ? stride - t0 * C : TT * C;
   // trials: grid.y is capped at YMAX, so a workgroup walks trials blockIdx.y + k gridDim.y
   for (int b = blockIdx.y; b < B; b += gridDim.y) {
-    const F* xb = x + (size_t)b * C * T;
     if (b != (int)blockIdx.y) __syncthreads();  // the previous trial's tile has been written out
-    // read: consecutive threads walk time within a channel row (coalesced)
-    for (int i = threadIdx.x; i < C * TT; i += QTHREADS) {
-      const int c = i / TT, t = i - c * TT;
-      if (t < nt) tile[t * C + c] = (int8_t)quantize_one<F>(xb[(size_t)c * T + t0 + t], s);
+    // the view starts at the trial's first byte rounded down to 4 (int8 trials are byte-aligned),
+    // so every load address below is 4-byte aligned; `d` is that rounding.  Its end is rounded up
+    // to a whole dword: the range check is per dword, so a dword holding the trial's last bytes
+    // would read as zeros otherwise.  The up to 3 bytes past the trial share that dword's page.
+    const uintptr_t a = (uintptr_t)(x + (size_t)b * C * T);
+    const int d = (int)(a & 3);
+    const int nrec = ((int)((size_t)C * T * sizeof(F)) + d + 3) & ~3;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)(a - d), (short)0, nrec, 0x00020000);
+    for (int c0 = wave; c0 < C; c0 += QWAVES * RCHUNK) {
+      Row4<F> v[RCHUNK];
+#pragma unroll
+      for (int k = 0; k < RCHUNK; k++) {
+        const int c = c0 + QWAVES * k;
+        if (c < C) v[k].load(r, d + (int)(((size_t)c * T + t0 + tl) * sizeof(F)));
+      }
+#pragma unroll
+      for (int k = 0; k < RCHUNK; k++) {
+        const int c = c0 + QWAVES * k;
+        if (c < C) {
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (tl + j < nt) tile[(tl + j) * C + c] = (int8_t)quantize_one<F>(v[k].get(j), s);
+        }
+      }
     }
+    if (last)  // the trial's pad bytes follow its last sample in the tile
+      for (int i = nt * C + threadIdx.x; i < nout; i += QTHREADS) tile[i] = 0;
     __syncthreads();
-    // write: the tile's nt * C bytes are contiguous in the output; dwords when aligned
-    int8_t* yb = y + (size_t)b * stride + (size_t)t0 * C;
-    const int nbytes = nt * C;
-    if (((t0 * C) & 3) == 0) {
-      const int nd = nbytes >> 2;
-      for (int i = threadIdx.x; i < nd; i += QTHREADS) ((int*)yb)[i] = ((const int*)tile)[i];
-      for (int i = (nd << 2) + threadIdx.x; i < nbytes; i += QTHREADS) yb[i] = tile[i];
-    } else {
-      for (int i = threadIdx.x; i < nbytes; i += QTHREADS) yb[i] = tile[i];
-    }
-    // trial pad bytes
-    if (t0 + TT >= T) {
-      int8_t* pad = y + (size_t)b * stride + (size_t)C * T;
-      for (int i = threadIdx.x; i < stride - C * T; i += QTHREADS) pad[i] = 0;
-    }
+    // the tile is contiguous in the output and both ends are 16-byte aligned (t0 C = 256 k C, the
+    // stride is a multiple of 16)
+    v4u* yb = (v4u*)(y + (size_t)b * stride + (size_t)t0 * C);
+    for (int i = threadIdx.x; i < nout / 16; i += QTHREADS) yb[i] = ((const v4u*)tile)[i];
   }
 }
 

@@ -79,6 +79,28 @@ def test_gpu_argmax_first_max(gpu, N, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_gpu_argmax4_alignment(gpu, shift):
+    """N = 4 takes four trials per thread when both buffers are 16-byte aligned (k_argmax4) and the
+    per-trial kernel otherwise; logits and classes starting `shift` trials into their buffers
+    cover both paths and every tail length."""
+    import torch
+
+    B = 4099
+    rng = np.random.default_rng(40 + shift)
+    z = rng.choice(np.array([-128, -1, 0, 5, 127], np.int8), size=(B + shift, 4))
+    zd = torch.from_numpy(z).to("cuda:0")
+    out = torch.full((B + shift,), -1, dtype=torch.int32, device="cuda:0")
+    L = lib.load()
+    rc = L.net_argmax_batch(zd.data_ptr() + 4 * shift, out.data_ptr() + 4 * shift, B, 4, 0, None)
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert np.array_equal(got[shift:], np.argmax(z[shift:], axis=1))
+    assert (got[:shift] == -1).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("clip_balanced", [False, True])
 def test_gpu_harness_vs_oracle(gpu, tmp_path, clip_balanced):
     bench = str(tmp_path / "benchmark.npz")

@@ -98,6 +98,11 @@ def test_pack_abi_checks():
     buf = np.zeros(64, np.int8)
     assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 1, 65, 10, 0, None) == lib.NET_ERR_INVALID
     assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 2**31, 22, 1125, 0, None) == lib.NET_ERR_INVALID
+    # the output must be 16-byte aligned (the tiles leave as 16-byte stores), and one trial's input
+    # must stay below 2 GiB (one buffer view)
+    base = (buf.ctypes.data + 15) // 16 * 16
+    assert L.net_pack_trials_i8(buf.ctypes.data, base + 4, 1, 2, 3, 0, None) == lib.NET_ERR_INVALID
+    assert L.net_quantize_input_f64(buf.ctypes.data, base, 1, 64, 2**22, 1.0, 0, None) == lib.NET_ERR_INVALID
 
 
 @pytest.mark.gpu
