@@ -702,7 +702,10 @@ int quantize_input(const F* x, int8_t* y, size_t B, int C, int T, F scale, int d
   const int stride = (int)(((size_t)C * T + 15) / 16 * 16);
   DeviceGuard guard(device);
   if (guard.err != hipSuccess) return hip_err(guard.err);
-  dim3 grid((T + quant::TT - 1) / quant::TT, (unsigned)std::min(B, (size_t)quant::YMAX));
+  // each workgroup walks a few trials, loading one trial ahead
+  constexpr size_t per = quant::qtrials<F>();
+  const size_t rows = std::min((B + per - 1) / per, (size_t)quant::YMAX);
+  dim3 grid((T + quant::TT - 1) / quant::TT, (unsigned)rows);
   hipLaunchKernelGGL(quant::k_quantize<F>, grid, dim3(quant::QTHREADS), 0, (hipStream_t)stream, x, y, C, T, stride, scale,
                      (int)B);
   return hip_err(hipGetLastError());

@@ -138,12 +138,13 @@ def test_gpu_int8_channel_major_end_to_end(gpu):
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [np.float32, np.float64])
 def test_gpu_quantize_past_grid_limit(gpu, dtype):
-    """B = 100,000 in one call (more trials than grid.y's 65,535: the kernel loops over trials)
-    == the NumPy restatement, for every trial."""
+    """B = 300,000 in one call == the NumPy restatement, for every trial.  A workgroup walks 2
+    (float) or 4 (int8) trials, so the grid wants 150,000 / 75,000 rows: past grid.y's 65,535
+    cap, where workgroups walk further trials, for every element type."""
     import torch
     from mibminet import lib
 
-    B, C, T, s = 100_000, 5, 70, 0.93
+    B, C, T, s = 300_000, 5, 70, 0.93
     rng = np.random.default_rng(100)
     x = rng.normal(scale=0.7, size=(B, C, T)).astype(dtype)
     got = lib.quantize_input_torch(torch.from_numpy(x).to("cuda:0"), s).cpu().numpy()
