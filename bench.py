@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--variant", default="canonical", choices=("canonical", "plain_bn", "clip_balanced"),
                     help="build variant the parameter blob selects: the canonical -DREORDER_BN build, the "
                          "plain-BN branches (layer2.c:139-210, layer4.c:91-133) or golden-model balanced clipping")
+    ap.add_argument("--layout", default="tc", choices=("tc", "ct"),
+                    help="input layout: tc = time-major batched trials [B][stride] (net_model_compute_batch), "
+                         "ct = channel-major [B][C][T] (net_model_compute_batch_ct, transposed inside the kernel)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed launches before the warmup steps (GPU clock ramp)")
@@ -198,14 +201,26 @@ def main():
     B = a.batch
     g = torch.Generator(device=dev)
     g.manual_seed(a.seed * 1000 + rank)
-    x = torch.randint(-128, 128, (B, stride), dtype=torch.int8, device=dev, generator=g)
-    x[:, cfg["C"] * cfg["T"]:] = 0
+    C, T = cfg["C"], cfg["T"]
+    if a.layout == "ct":
+        xc = torch.randint(-128, 128, (B, C, T), dtype=torch.int8, device=dev, generator=g)
+        x = torch.zeros((B, stride), dtype=torch.int8, device=dev)  # the same trials, time-major
+        x[:, : C * T] = xc.transpose(1, 2).reshape(B, C * T)         # (CPU baseline and --pcie)
+    else:
+        x = torch.randint(-128, 128, (B, stride), dtype=torch.int8, device=dev, generator=g)
+        x[:, C * T:] = 0
     y = torch.empty((B, 4), dtype=torch.int8, device=dev)
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
+    ct_fn = lib.load().net_model_compute_batch_ct
 
     def step():
-        lib.model_compute_batch(x.data_ptr(), y.data_ptr(), B, local, sp)
+        if a.layout == "ct":
+            rc = ct_fn(xc.data_ptr(), y.data_ptr(), B, local, sp)
+            if rc:
+                raise lib.NetError(rc, "net_model_compute_batch_ct")
+        else:
+            lib.model_compute_batch(x.data_ptr(), y.data_ptr(), B, local, sp)
 
     # settle (untimed, before the W warmup steps): from idle the GPU clock needs some tens of ms
     # of load to reach its steady state; without this the first ~50 ms run about 7 % slower
@@ -269,14 +284,15 @@ def main():
             # (tools/collect_profile.py), per config under "configs"
             tj = json.load(open(a.traffic_json))
             tc = tj.get("configs", {}).get(a.config, tj if tj.get("config") == a.config else {})
-            if tc.get("batch") == B and a.variant == "canonical":
+            if tc.get("batch") == B and a.variant == "canonical" and a.layout == "tc":
                 traffic = tc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
         value = world * B * a.steps / elapsed
         out = {
-            "metric": (METRIC if a.config == "b22" and a.variant == "canonical"
-                       else f"EEG trials/sec ({cfg['name']}, {a.variant} build) at batch {B}"),
+            "metric": (METRIC if a.config == "b22" and a.variant == "canonical" and a.layout == "tc"
+                       else f"EEG trials/sec ({cfg['name']}, {a.variant} build, "
+                            f"{'channel-major' if a.layout == 'ct' else 'time-major'} input) at batch {B}"),
             "value": value,
             "unit": "trials/s",
             "n_gpus": world,
@@ -290,13 +306,15 @@ def main():
             "dtype": "int8",
             "data": "synthetic (uniform int8 EEG generated on device; seeded synthetic integer weights)",
             "config": {"workload": cfg["name"], "variant": a.variant, "C": cfg["C"], "T": cfg["T"], "batch_per_gpu": B,
+                       "input_layout": ("[B][C][T] channel-major (net_model_compute_batch_ct)" if a.layout == "ct"
+                                        else "[B][T][C] time-major, 16-byte trial stride (net_model_compute_batch)"),
                        "global_batch": world * B, "weight_bits": cfg["wbits"],
                        "parallelism": f"dp{world} static batch split, no collectives",
                        "grid": info["grid"], "threads": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d>>" % (cfg["C"], cfg["T"], a.variant != "plain_bn",
-                                                                          a.variant == "clip_balanced"),
+                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d>>" % (cfg["C"], cfg["T"], a.variant != "plain_bn",
+                                                                                a.variant == "clip_balanced", a.layout == "ct"),
                          "avg_kernel_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes_trial * B},
             "cpu_baseline": None,

@@ -109,6 +109,13 @@ int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device);
 /* Same, enqueued on `stream` (a hipStream_t of `device`, NULL = null stream), no host sync. */
 int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream);
 
+/* Channel-major trials (SURVEY §8(b)'s batched signature; the layout of the reference's
+ * input.npz before gen_input_header.py:74 transposes it): x: DEVICE pointer to B trials
+ * [B][C][T] int8, contiguous (trial stride C*T bytes, any alignment); y: DEVICE pointer [B][N],
+ * 4-byte aligned.  The same fused forward, with each layer-1 block transposed through LDS inside
+ * the kernel (no separate pack pass).  Enqueued on `stream` (NULL = null stream), no host sync. */
+int net_model_compute_batch_ct(const int8_t* x, int8_t* y, size_t B, int device, void* stream);
+
 /* Several devices from one host thread (static split, no collectives): shard i is
  * x[i] / y[i] / B[i] on devices[i] (DEVICE pointers of that device).  Every shard is enqueued
  * before any is waited for, so the devices run concurrently.  streams == NULL: each device's null

@@ -84,6 +84,7 @@ struct SmallParams {
 // Operand fragments and requantisation constants, built by the host from the net.h arrays.
 struct DevParams {
   v4i l1_wfrag[2][64];      // layer-1 B operand per N-tile and lane
+  v4i l1_wfrag_ct[2][64];   // the same for the channel-major staging's window order (Cfg::SG)
   int l1_cinit[2][16];      // offset + FMAGIC_I per N-tile column
   float l1_r[2][16];        // reciprocal per N-tile column
   float l1_c[2][16];        // -(1.5 * 2^23) * r, exact

@@ -89,11 +89,12 @@ constexpr L1Split l1_split(int nb1) {
   return best;
 }
 
-template <int C_, int T_, bool RB_ = true, bool CB_ = false>
+template <int C_, int T_, bool RB_ = true, bool CB_ = false, bool CT_ = false>
 struct Cfg {
   static constexpr int C = C_, T = T_;
   static constexpr bool RB = RB_;                       // -DREORDER_BN variant (canonical)
   static constexpr bool CB = CB_;                       // golden-model clip_balanced: clip to [-127, 127]
+  static constexpr bool CT = CT_;                       // channel-major [C][T] trials, staged in LDS (layer1)
   static constexpr int LO = CB ? -127 : -128;           // lower clip bound of every requant
   static constexpr int P = (C <= 32) ? 2 : 1;          // samples per 64-byte L1 window
   static constexpr int GS = P * C;                      // bytes per time group
@@ -118,7 +119,18 @@ struct Cfg {
   static constexpr int NPOS = cmax(cmax(32 + 16 * P * NB1, 32 * (NB2 - 1) + 96), 1024 * MT + 64);
   static constexpr int PLANE = align16((NPOS + P - 1) / P);
   static constexpr int Y1ROW = P * PLANE;
-  static constexpr int XTRIAL = align16(T * C);         // batched trial stride (bytes)
+  // batched trial stride (bytes): time-major trials are padded to 16 bytes, channel-major ones
+  // are the caller's contiguous [B][C][T]
+  static constexpr int XTRIAL = CT ? C * T : align16(T * C);
+  // channel-major staging (layer1, CT): one layer-1 block per wave, time group j at SG j.  P == 2:
+  // window slot 2c + p = channel c of the group's sample p (44 bytes for C = 22); P == 1: slot c.
+  // The last group's window runs 16 bytes past the block (zero weights meet them).
+  static constexpr int SG = P == 2 ? align16(2 * C) : 64;
+  static constexpr int STG = 16 * SG + 16;
+#ifndef MIB_CT_NSTG
+#define MIB_CT_NSTG 2
+#endif
+  static constexpr int NSTG = MIB_CT_NSTG;               // staging buffers per wave (pipelined)
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   // layer 3: tile 1 = the first L3C blocks of both filters side by side (one 16x16x64 MFMA),
   // tile 2 = the L3R outputs past 128, four per column in register 0 only (layer3)
@@ -146,7 +158,8 @@ struct Cfg {
   static constexpr int OFF_LT = align16(OFF_SP + (int)sizeof(SmallParams));   // per-lane offsets
   static constexpr int OFF_L45 = OFF_LT + 64 * 48;                            // layer-4/5 lane offsets
   static constexpr int OFF_L2T = OFF_L45 + 64 * 32;                           // tail band fragments
-  static constexpr int LDS = OFF_L2T + (TB > 0 ? NWAVES * 3 * 64 * 16 : 0);
+  static constexpr int OFF_STG = OFF_L2T + (TB > 0 ? NWAVES * 3 * 64 * 16 : 0);   // CT staging
+  static constexpr int LDS = OFF_STG + (CT ? NWAVES * NSTG * STG : 0);
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
   static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
   static_assert(T64 >= 1, "T >= 64");
@@ -340,6 +353,16 @@ typedef __amdgpu_buffer_rsrc_t Rsrc;
 // the trial's end) from memory.  trials_left <= 0: an empty view.
 template <class K>
 __device__ __forceinline__ Rsrc trial_rsrc(const int8_t* xt, int trials_left, int wave) {
+  if constexpr (K::CT) {
+    // channel-major: a wave's blocks lie in every channel row, so the view is the whole trial;
+    // row segments running past T read the next row (samples >= T, whose outputs are masked).
+    // Rows start at any byte, and the range check is per dword OF THE LOAD (tools/ct_probe.hip):
+    // a dword straddling num_records reads as zeros.  So the view runs 3 bytes past the trial,
+    // into the next trial's bytes, except for the batch's last trial, whose straddling dword is
+    // completed by byte loads (ct_tail).
+    const int n = trials_left <= 0 ? 0 : trials_left == 1 ? K::C * K::T : K::C * K::T + 3;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)xt, (short)0, n, 0x00020000);
+  }
   const int wb = l1_start<K>(wave) * 16 * K::GS;  // byte offset of the wave's first block
   const int own = min(l1_count<K>(wave) * 16 * K::GS, K::XTRIAL - wb);
   const int nrec = trials_left <= 0 ? 0 : max(own, 0);
@@ -347,7 +370,17 @@ __device__ __forceinline__ Rsrc trial_rsrc(const int8_t* xt, int trials_left, in
 }
 
 template <class K>
-__device__ __forceinline__ int lane_xoff(int lane) {
+__device__ __forceinline__ int lane_xoff(int lane, int wave) {
+  if constexpr (K::CT) {
+    // channel-major: lane (c, h) (P == 2) or c (P == 1) reads 16 samples of channel row c; block
+    // slot i adds 16 P i samples.  Lanes past the rows read zeros without a fetch.
+    const int c = K::P == 2 ? lane >> 1 : lane, h = K::P == 2 ? lane & 1 : 0;
+    if (c >= K::C) return (int)0x80000000u;
+#ifdef MIB_DIAG_CT_ALIGNED
+    return (c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h) & ~15;  // timing proxy (results wrong)
+#endif
+    return c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h;
+  }
 #ifndef MIB_NO_ZERO_PAD_LANES
   // A lane whose 16-byte chunk lies wholly past the group's P * C bytes (C = 22: bytes 48..63)
   // only meets zero weights: it reads past num_records instead (offset >= 2^31 > any
@@ -361,8 +394,72 @@ __device__ __forceinline__ int lane_xoff(int lane) {
 template <class K>
 __device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * 16 * K::GS, 0, 2 /* nt */);
+  // block stride: 16 time groups (time-major) or 16 P samples of a row (channel-major)
+  constexpr int BSTR = K::CT ? 16 * K::P : 16 * K::GS;
+#ifndef MIB_CT_AUX
+#define MIB_CT_AUX 0
+#endif
+  // cache policy: nt (2) for the time-major stream; none for channel-major, whose 128-byte lines
+  // are read by several block loads of a wave (nt: +40 %, tools/ab.py)
+  constexpr int AUX = K::CT ? MIB_CT_AUX : 2;
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * BSTR, 0, AUX);
   return (v4i)v;
+}
+
+// The batch's last trial, channel-major: the one dword of the view that holds the trial's last
+// byte(s) and straddles its end read as zeros (trial_rsrc); the lane holding it reloads those 1-3
+// bytes one at a time (byte loads are range-checked per byte).  Once per launch.
+template <class K>
+__device__ __forceinline__ v4i ct_tail(v4i a, Rsrc r, int o) {
+  constexpr int N = K::C * K::T;
+  if (o < N && N < o + 16 && ((N - o) & 3)) {
+    const int k0 = (N - o) & ~3;
+    unsigned w = 0;
+    for (int m = 0; o + k0 + m < N; m++)
+      w |= (unsigned)__builtin_amdgcn_raw_buffer_load_b8(r, o + k0 + m, 0, 0) << (8 * m);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (4 * q == k0) a[q] = (int)w;
+  }
+  return a;
+}
+
+// Channel-major staging of one layer-1 block (K::CT): the raw 16 bytes of a lane (16 samples of
+// channel c) go to the wave's staging area in the window layout of Cfg::SG, from where the block's
+// MFMA A fragment is read as one ds_read_b128.  P == 2: sample pair (2i, 2i + 1) of the lane is
+// window slots 2c, 2c + 1 of time group 8h + i: eight 2-byte stores straight from the loaded dwords
+// (low and high halves).  P == 1: sixteen byte stores (slot c of rows 0..15).  LDS accesses of a
+// wave complete in order, so the A read sees these stores and the next block's stores follow it.
+__device__ __forceinline__ void wave_sync_lds() {
+  // orders this wave's LDS accesses across lanes for the compiler (no instruction is emitted):
+  // without it, a lane that stores nothing may be given its previous read's value instead of a
+  // new read (the other lanes' stores are invisible to the per-thread memory model)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class K>
+__device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
+  wave_sync_lds();  // the previous block's A reads precede these stores
+  if constexpr (K::P == 2) {
+    if (lane < 2 * K::C) {
+      int8_t* p = stg + 8 * K::SG * (lane & 1) + 2 * (lane >> 1);
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const unsigned w = (unsigned)raw[i >> 1];
+        *(unsigned short*)(p + K::SG * i) = (unsigned short)((i & 1) ? (w >> 16) : w);
+      }
+    }
+  } else {
+    if (lane < K::C) {
+      int8_t* p = stg + lane;
+#pragma unroll
+      for (int i = 0; i < 16; i++) p[K::SG * i] = (int8_t)((unsigned)raw[i >> 2] >> (8 * (i & 3)));
+    }
+  }
+  wave_sync_lds();
+  return *(const v4i*)(stg + K::SG * (lane & 15) + 16 * (lane >> 4));
 }
 
 template <class K>
@@ -381,8 +478,8 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
 #pragma unroll
   for (int t = 0; t < K::P; t++) {
     L1Tile& T = R.tile(t);
-    R.xoff = lane_xoff<K>(lane);
-    T.wf = prm->l1_wfrag[t][lane];
+    R.xoff = lane_xoff<K>(lane, wave);
+    T.wf = K::CT ? prm->l1_wfrag_ct[t][lane] : prm->l1_wfrag[t][lane];
     T.ci = prm->l1_cinit[t][lane & 15];
     T.rr = prm->l1_r[t][lane & 15];
     T.cc = prm->l1_c[t][lane & 15];
@@ -477,17 +574,38 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
 // Layer 1: x[T][C] (HBM, via R.pf) -> y1 rows (LDS, position 32 + t).  Prefetches the next
 // trial's fragments (rnext) into R.pf once the current ones are consumed.
 template <class K>
-__device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, Regs<K>& R, int wave, int lane) {
+__device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, Regs<K>& R, int wave, int lane,
+                                       bool last_trial = false) {
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
   v4i xa[NX > 0 ? NX : 1];
 #pragma unroll
   for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
+  // channel-major: block i + 1 is staged (stores and A read, buffer (i + 1) & 1) before block i's
+  // MFMAs, so the staging latency passes under them
+  int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::NSTG * K::STG;
+  auto staged = [&](int i) -> v4i {
+    v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
+    if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
+#ifndef MIB_DIAG_CT_NOSTAGE
+    a = stage_block<K>(a, stg + (i % K::NSTG) * K::STG, lane);
+#endif
+    return a;
+  };
+  v4i an = {0, 0, 0, 0};
+  if constexpr (K::CT)
+    if (n > 0) an = staged(0);
 #pragma unroll
   for (int i = 0; i < K::NBW; i++) {
     if (i < n) {  // wave-uniform
       const int blk = l1_blk<K>(wave, i);
-      v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
+      v4i a;
+      if constexpr (K::CT) {
+        a = an;
+        if (i + 1 < n) an = staged(i + 1 < K::NBW ? i + 1 : 0);
+      } else {
+        a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
+      }
       if (blk == K::NB1 - 1) {  // the trial's last block: samples >= T are masked
         l1_block<K, true>(a, blk, smem_y1, R, lane);
       } else {
@@ -886,7 +1004,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
 #endif
     MIB_STAMP(7)
     __builtin_amdgcn_s_setprio(PRIO_L1);
-    layer1<K>(rc, rn, smem + K::OFF_Y1, R, wave, lane);
+    layer1<K>(rc, rn, smem + K::OFF_Y1, R, wave, lane, MIB_TRIALS_LEFT(b) == 1);
     __builtin_amdgcn_s_setprio(0);
     MIB_STAMP(0)
     // the lane table is read before barrier A, so its LDS latency hides in the barrier wait

@@ -332,6 +332,14 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         bytes[jj] = (int8_t)((c >= 0 && c < C) ? w1(f, c) : 0);
       }
       std::memcpy(&dp.l1_wfrag[t][lane], bytes, 16);
+      // channel-major staging (forward_wg.hpp, stage_block): P == 2 window slot 2c + p holds
+      // channel c of sample p; P == 1 is the same slot order as above
+      for (int jj = 0; jj < 16; jj++) {
+        const int k = 16 * g + jj;
+        const int c = P == 2 ? k >> 1 : k, pk = P == 2 ? k & 1 : 0;
+        bytes[jj] = (int8_t)((c < C && pk == p) ? w1(f, c) : 0);
+      }
+      std::memcpy(&dp.l1_wfrag_ct[t][lane], bytes, 16);
     }
     for (int j = 0; j < 16; j++) {
       const int f = P == 2 ? 8 * t + (j >> 1) : j;
@@ -460,19 +468,19 @@ Variant variant_of(const HostParams& hp) {
   return v;
 }
 
-template <int C, int T, class F>
+template <int C, int T, bool CT, class F>
 int with_variant(const Variant& v, F&& f) {
-  if (v.rb) return v.cb ? f(wg::Cfg<C, T, true, true>{}) : f(wg::Cfg<C, T, true, false>{});
-  return v.cb ? f(wg::Cfg<C, T, false, true>{}) : f(wg::Cfg<C, T, false, false>{});
+  if (v.rb) return v.cb ? f(wg::Cfg<C, T, true, true, CT>{}) : f(wg::Cfg<C, T, true, false, CT>{});
+  return v.cb ? f(wg::Cfg<C, T, false, true, CT>{}) : f(wg::Cfg<C, T, false, false, CT>{});
 }
 
-// Calls f(K{}) with the kernel configuration K of the variant.
-template <class F>
+// Calls f(K{}) with the kernel configuration K of the variant (CT: channel-major input trials).
+template <bool CT = false, class F>
 int dispatch(const Variant& v, F&& f) {
   switch (v.shape) {
-    case 0: return with_variant<22, 1125>(v, f);
-    case 1: return with_variant<64, 1000>(v, f);
-    case 2: return with_variant<64, 480>(v, f);
+    case 0: return with_variant<22, 1125, CT>(v, f);
+    case 1: return with_variant<64, 1000, CT>(v, f);
+    case 2: return with_variant<64, 480, CT>(v, f);
     default: return NET_ERR_UNSUPPORTED;
   }
 }
@@ -630,8 +638,9 @@ int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_
 }
 
 int launch_forward(const Variant& v, DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y,
-                   size_t B, hipStream_t st, int32_t* info = nullptr) {
-  return dispatch(v, [&](auto k) { return launch_forward_t<decltype(k)>(ds, p, x, y, B, st, info); });
+                   size_t B, hipStream_t st, int32_t* info = nullptr, bool ct = false) {
+  auto f = [&](auto k) { return launch_forward_t<decltype(k)>(ds, p, x, y, B, st, info); };
+  return ct ? dispatch<true>(v, f) : dispatch<false>(v, f);
 }
 
 int launch_layer(const Variant& v, const DevParams* p, const int8_t* in, int8_t* out, int stage) {
@@ -808,9 +817,12 @@ int net_set_device(int device) {
   return NET_OK;
 }
 
-int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream) {
+namespace {
+// ct: channel-major trials [B][C][T] (any alignment, trial stride C T bytes); otherwise the
+// time-major batched layout (16-byte aligned, stride net_trial_stride())
+int batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream, bool ct) {
   if ((!x || !y) && B) return NET_ERR_INVALID;
-  if (((uintptr_t)x & 15) != 0 || ((uintptr_t)y & 3) != 0) return NET_ERR_INVALID;
+  if ((!ct && ((uintptr_t)x & 15) != 0) || ((uintptr_t)y & 3) != 0) return NET_ERR_INVALID;
   if (device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
@@ -823,7 +835,16 @@ int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int devi
   if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
-  return launch_forward(v, ds, ds.cur, x, y, B, (hipStream_t)stream);
+  return launch_forward(v, ds, ds.cur, x, y, B, (hipStream_t)stream, nullptr, ct);
+}
+}  // namespace
+
+int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream) {
+  return batch_async(x, y, B, device, stream, false);
+}
+
+int net_model_compute_batch_ct(const int8_t* x, int8_t* y, size_t B, int device, void* stream) {
+  return batch_async(x, y, B, device, stream, true);
 }
 
 int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, float scale, int device, void* stream) {

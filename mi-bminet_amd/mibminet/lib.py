@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "net_params_dims", "net_params_unload", "net_trial_stride", "net_model_compute_batch",
     "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
-    "net_pack_trials_i8", "net_model_compute_batch_multi",
+    "net_pack_trials_i8", "net_model_compute_batch_multi", "net_model_compute_batch_ct",
 )
 
 
@@ -102,6 +102,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_pack_trials_i8.restype = i
     L.net_argmax_batch.argtypes = [vp, vp, sz, i, i, vp]
     L.net_argmax_batch.restype = i
+    L.net_model_compute_batch_ct.argtypes = [vp, vp, sz, i, vp]
+    L.net_model_compute_batch_ct.restype = i
     _lib = L
     return L
 
@@ -249,6 +251,23 @@ def forward_torch(x, params: Optional[ParamSet] = None, stream=None):
     y = torch.empty((B, d.N), dtype=torch.int8, device=x.device)
     s = torch.cuda.current_stream(x.device) if stream is None else stream
     model_compute_batch(x.data_ptr(), y.data_ptr(), B, x.device.index or 0, s.cuda_stream)
+    return y
+
+
+def forward_ct_torch(x, stream=None):
+    """net_model_compute_batch_ct: x is a CUDA/HIP int8 tensor [B][C][T] (channel-major, the
+    reference's input.npz layout; any byte alignment) -> logits [B][N] tensor, with no separate
+    transpose pass."""
+    import torch
+
+    d = _dims()
+    if x.dtype != torch.int8 or not x.is_cuda or not x.is_contiguous() or tuple(x.shape[1:]) != (d.C, d.T):
+        raise ValueError(f"x must be a contiguous int8 device tensor [B][{d.C}][{d.T}]")
+    B = x.shape[0]
+    y = torch.empty((B, d.N), dtype=torch.int8, device=x.device)
+    s = torch.cuda.current_stream(x.device) if stream is None else stream
+    _check(load().net_model_compute_batch_ct(x.data_ptr(), y.data_ptr(), B, x.device.index or 0, s.cuda_stream),
+           "net_model_compute_batch_ct")
     return y
 
 

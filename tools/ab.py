@@ -27,9 +27,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variant", default="canonical", choices=("canonical", "plain_bn", "clip_balanced"))
+    ap.add_argument("--ct", action="store_true", help="channel-major input (net_model_compute_batch_ct)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
-    C, T = {"b22": (22, 1125), "c64": (64, 1000)}[a.cfg]
+    C, T = {"b22": (22, 1125), "c64": (64, 1000), "p64": (64, 480)}[a.cfg]
     blob = ParamSet.synthetic(seed=1, C=C, T=T, reorder_bn=a.variant != "plain_bn",
                               clip_balanced=a.variant == "clip_balanced").to_blob()
     libs = []
@@ -39,10 +40,13 @@ def main():
         L.net_trial_stride.restype = ctypes.c_size_t
         L.net_model_compute_batch_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                                     ctypes.c_int, ctypes.c_void_p]
+        L.net_model_compute_batch_ct.argtypes = L.net_model_compute_batch_async.argtypes
+        if a.ct:
+            L.net_model_compute_batch_async = L.net_model_compute_batch_ct
         rc = L.net_params_load(blob, len(blob))
         assert rc == 0, (p, rc)
         libs.append(L)
-    stride = libs[0].net_trial_stride()
+    stride = C * T if a.ct else libs[0].net_trial_stride()
     x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0")
     y = torch.empty((a.B, 4), dtype=torch.int8, device="cuda:0")
     st = torch.cuda.current_stream()
