@@ -452,11 +452,30 @@ __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
       }
     }
   } else {
+#ifdef MIB_CT_P1_B8
     if (lane < K::C) {
       int8_t* p = stg + lane;
 #pragma unroll
       for (int i = 0; i < 16; i++) p[K::SG * i] = (int8_t)((unsigned)raw[i >> 2] >> (8 * (i & 3)));
     }
+#else
+    // channel pairs (c, c ^ 1) trade dwords (DPP quad_perm [1,0,3,2]); one v_perm then forms the
+    // (channel c & ~1, c | 1) byte pairs of two samples: the even lane those of samples 4k, 4k + 2,
+    // the odd lane 4k + 1, 4k + 3.  Eight 2-byte stores per lane instead of sixteen byte stores.
+    static_assert(K::C % 2 == 0, "channel pairs");
+    const unsigned sel = (lane & 1) ? 0x03070105u : 0x06020400u;
+    int8_t* p = stg + (lane & ~1) + K::SG * (lane & 1);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const unsigned d = (unsigned)raw[k];
+      const unsigned q = (unsigned)__builtin_amdgcn_mov_dpp((int)d, 0xB1, 0xF, 0xF, false);
+      const unsigned w = __builtin_amdgcn_perm(q, d, sel);
+      if (lane < K::C) {
+        *(unsigned short*)(p + K::SG * 4 * k) = (unsigned short)w;
+        *(unsigned short*)(p + K::SG * (4 * k + 2)) = (unsigned short)(w >> 16);
+      }
+    }
+#endif
   }
   wave_sync_lds();
   return *(const v4i*)(stg + K::SG * (lane & 15) + 16 * (lane >> 4));
