@@ -511,6 +511,9 @@ struct DeviceState {
   uint64_t tick = 0;
   int8_t* d_in = nullptr;       // single-trial scratch
   int8_t* d_out = nullptr;
+  int8_t* h_in = nullptr;       // pinned host staging of the single-trial copies
+  int8_t* h_out = nullptr;
+  hipStream_t st = nullptr;     // the single-trial path's own non-blocking stream
   size_t scratch = 0;
   int cus = 0;
 };
@@ -603,15 +606,27 @@ int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
   return NET_OK;
 }
 
+// Single-trial scratch: device buffers, pinned host staging (the copies run as DMA without the
+// runtime's pageable bounce) and a non-blocking stream (no implicit sync with the null stream).
 int ensure_scratch(DeviceState& ds, size_t bytes) {
+  if (!ds.st) {
+    hipError_t e = hipStreamCreateWithFlags(&ds.st, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      ds.st = nullptr;
+      return hip_err(e);
+    }
+  }
   if (ds.scratch >= bytes) return NET_OK;
   if (ds.d_in) (void)hipFree(ds.d_in);
   if (ds.d_out) (void)hipFree(ds.d_out);
-  ds.d_in = ds.d_out = nullptr;
+  if (ds.h_in) (void)hipHostFree(ds.h_in);
+  if (ds.h_out) (void)hipHostFree(ds.h_out);
+  ds.d_in = ds.d_out = ds.h_in = ds.h_out = nullptr;
   ds.scratch = 0;
   hipError_t e = hipMalloc((void**)&ds.d_in, bytes);
-  if (e != hipSuccess) return hip_err(e);
-  e = hipMalloc((void**)&ds.d_out, bytes);
+  if (e == hipSuccess) e = hipMalloc((void**)&ds.d_out, bytes);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&ds.h_in, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&ds.h_out, bytes, hipHostMallocMapped | hipHostMallocCoherent);
   if (e != hipSuccess) return hip_err(e);
   ds.scratch = bytes;
   return NET_OK;
@@ -643,9 +658,9 @@ int launch_forward(const Variant& v, DeviceState& ds, const DevParams* p, const 
   return ct ? dispatch<true>(v, f) : dispatch<false>(v, f);
 }
 
-int launch_layer(const Variant& v, const DevParams* p, const int8_t* in, int8_t* out, int stage) {
+int launch_layer(const Variant& v, const DevParams* p, const int8_t* in, int8_t* out, int stage, hipStream_t st) {
   return dispatch(v, [&](auto k) {
-    hipLaunchKernelGGL(wg::k_layer<decltype(k)>, dim3(1), dim3(wg::NTHREADS), 0, 0, p, in, out, stage);
+    hipLaunchKernelGGL(wg::k_layer<decltype(k)>, dim3(1), dim3(wg::NTHREADS), 0, st, p, in, out, stage);
     return hip_err(hipGetLastError());
   });
 }
@@ -667,13 +682,14 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
   int rc = ensure_device(ds, dev, s);
   if (rc) return rc;
   const size_t xs = trial_stride(d);
+  rc = ensure_scratch(ds, xs > (size_t)d.F1 * d.T_ALIGN() ? xs + 64 : (size_t)d.F1 * d.T_ALIGN() + 64);
+  if (rc) return rc;
   size_t in_bytes, out_bytes;
-  std::vector<int8_t> hin;
   switch (stage) {
     case 0:
-    case 1: {  // reference input [T][C_ALIGN] -> packed [T][C]
-      hin.assign(xs, 0);
-      for (int t = 0; t < d.T; t++) std::memcpy(&hin[(size_t)t * d.C], in + (size_t)t * d.C_ALIGN(), d.C);
+    case 1: {  // reference input [T][C_ALIGN] -> packed [T][C], straight into the pinned staging
+      for (int t = 0; t < d.T; t++) std::memcpy(ds.h_in + (size_t)t * d.C, in + (size_t)t * d.C_ALIGN(), d.C);
+      std::memset(ds.h_in + (size_t)d.T * d.C, 0, xs - (size_t)d.T * d.C);
       in_bytes = xs;
       out_bytes = stage == 0 ? (size_t)d.N : (size_t)d.F1 * d.T_ALIGN();
       break;
@@ -685,18 +701,41 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
     case 6: in_bytes = out_bytes = (size_t)d.F2 * d.T8_ALIGN(); break;
     default: return NET_ERR_INVALID;
   }
-  rc = ensure_scratch(ds, xs > (size_t)d.F1 * d.T_ALIGN() ? xs + 64 : (size_t)d.F1 * d.T_ALIGN() + 64);
-  if (rc) return rc;
-  hipError_t e = hipMemcpy(ds.d_in, hin.empty() ? (const void*)in : (const void*)hin.data(), in_bytes,
-                           hipMemcpyHostToDevice);
+  if (stage > 1) std::memcpy(ds.h_in, in, in_bytes);
+  hipError_t e;
+#ifdef MIB_SINGLE_COPIES
+  e = hipMemcpyAsync(ds.d_in, ds.h_in, in_bytes, hipMemcpyHostToDevice, ds.st);
   if (e != hipSuccess) return hip_err(e);
+  int8_t* kin = ds.d_in;
+  int8_t* kout = ds.d_out;
+#else
+  // zero copy: the kernel reads the trial from the pinned staging and writes its result there
+  // (one launch per call instead of copy + launch + copy)
+  int8_t* kin = nullptr;
+  int8_t* kout = nullptr;
+  e = hipHostGetDevicePointer((void**)&kin, ds.h_in, 0);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&kout, ds.h_out, 0);
+  if (e != hipSuccess) return hip_err(e);
+#endif
   if (stage == 0)
-    rc = launch_forward(v, ds, ds.cur, ds.d_in, ds.d_out, 1, 0);
+    rc = launch_forward(v, ds, ds.cur, kin, kout, 1, ds.st);
   else
-    rc = launch_layer(v, ds.cur, ds.d_in, ds.d_out, stage);
-  if (rc) return rc;
-  e = hipMemcpy(out, ds.d_out, out_bytes, hipMemcpyDeviceToHost);
-  return hip_err(e);
+    rc = launch_layer(v, ds.cur, kin, kout, stage, ds.st);
+  if (rc) {
+    (void)hipStreamSynchronize(ds.st);  // a copy may still read the staging
+    return rc;
+  }
+#ifdef MIB_SINGLE_COPIES
+  e = hipMemcpyAsync(ds.h_out, ds.d_out, out_bytes, hipMemcpyDeviceToHost, ds.st);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(ds.st);
+    return hip_err(e);
+  }
+#endif
+  e = hipStreamSynchronize(ds.st);
+  if (e != hipSuccess) return hip_err(e);
+  std::memcpy(out, ds.h_out, out_bytes);
+  return NET_OK;
 }
 
 template <class F>
