@@ -127,10 +127,6 @@ struct Cfg {
   // The last group's window runs 16 bytes past the block (zero weights meet them).
   static constexpr int SG = P == 2 ? align16(2 * C) : 64;
   static constexpr int STG = 16 * SG + 16;
-#ifndef MIB_CT_NSTG
-#define MIB_CT_NSTG 2
-#endif
-  static constexpr int NSTG = MIB_CT_NSTG;               // staging buffers per wave (pipelined)
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   // layer 3: tile 1 = the first L3C blocks of both filters side by side (one 16x16x64 MFMA),
   // tile 2 = the L3R outputs past 128, four per column in register 0 only (layer3)
@@ -159,7 +155,7 @@ struct Cfg {
   static constexpr int OFF_L45 = OFF_LT + 64 * 48;                            // layer-4/5 lane offsets
   static constexpr int OFF_L2T = OFF_L45 + 64 * 32;                           // tail band fragments
   static constexpr int OFF_STG = OFF_L2T + (TB > 0 ? NWAVES * 3 * 64 * 16 : 0);   // CT staging
-  static constexpr int LDS = OFF_STG + (CT ? NWAVES * NSTG * STG : 0);
+  static constexpr int LDS = OFF_STG + (CT ? NWAVES * STG : 0);
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
   static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
   static_assert(T64 >= 1, "T >= 64");
@@ -376,9 +372,6 @@ __device__ __forceinline__ int lane_xoff(int lane, int wave) {
     // slot i adds 16 P i samples.  Lanes past the rows read zeros without a fetch.
     const int c = K::P == 2 ? lane >> 1 : lane, h = K::P == 2 ? lane & 1 : 0;
     if (c >= K::C) return (int)0x80000000u;
-#ifdef MIB_DIAG_CT_ALIGNED
-    return (c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h) & ~15;  // timing proxy (results wrong)
-#endif
     return c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h;
   }
 #ifndef MIB_NO_ZERO_PAD_LANES
@@ -395,14 +388,13 @@ template <class K>
 __device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   // block stride: 16 time groups (time-major) or 16 P samples of a row (channel-major)
-  constexpr int BSTR = K::CT ? 16 * K::P : 16 * K::GS;
 #ifndef MIB_CT_AUX
 #define MIB_CT_AUX 0
 #endif
   // cache policy: nt (2) for the time-major stream; none for channel-major, whose 128-byte lines
   // are read by several block loads of a wave (nt: +40 %, tools/ab.py)
   constexpr int AUX = K::CT ? MIB_CT_AUX : 2;
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * BSTR, 0, AUX);
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * (K::CT ? 16 * K::P : 16 * K::GS), 0, AUX);
   return (v4i)v;
 }
 
@@ -424,12 +416,8 @@ __device__ __forceinline__ v4i ct_tail(v4i a, Rsrc r, int o) {
   return a;
 }
 
-// Channel-major staging of one layer-1 block (K::CT): the raw 16 bytes of a lane (16 samples of
-// channel c) go to the wave's staging area in the window layout of Cfg::SG, from where the block's
-// MFMA A fragment is read as one ds_read_b128.  P == 2: sample pair (2i, 2i + 1) of the lane is
-// window slots 2c, 2c + 1 of time group 8h + i: eight 2-byte stores straight from the loaded dwords
-// (low and high halves).  P == 1: sixteen byte stores (slot c of rows 0..15).  LDS accesses of a
-// wave complete in order, so the A read sees these stores and the next block's stores follow it.
+// Channel-major staging (K::CT).  The hardware executes a wave's LDS accesses in order, so an A
+// read sees the stores before it and the next stores follow it; wave_sync_lds tells the compiler.
 __device__ __forceinline__ void wave_sync_lds() {
   // orders this wave's LDS accesses across lanes for the compiler (no instruction is emitted):
   // without it, a lane that stores nothing may be given its previous read's value instead of a
@@ -439,46 +427,51 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// the MFMA A fragment of the block staged at stg (time group j = lane & 15, bytes 16 (lane >> 4))
+template <class K>
+__device__ __forceinline__ v4i staged_a(const int8_t* stg, int lane) {
+  return *(const v4i*)(stg + K::SG * (lane & 15) + 16 * (lane >> 4));
+}
+
+// One layer-1 block: the lane's 16 samples of channel c go to the wave's staging area in the
+// window layout of Cfg::SG and come back as the block's MFMA A fragment (one ds_read_b128).
+//  P == 2 (window slot 2c + p = channel c of the group's sample p): lanes (c, h) and (c ^ 1, h)
+//    trade dwords by DPP (partner lane L ^ 2), and one v_perm forms a time group's 4 bytes of the
+//    channel pair; 4 dword stores per lane (-4.9 % against 8 two-byte stores straight from the
+//    loaded dwords; tools/ab.py --ct).
+//  P == 1 (slot c): a 4 x 4 byte transpose inside each lane quad (channels c0 .. c0 + 3, dword k
+//    = samples 4k .. 4k + 3) in two DPP + v_perm stages (partner L ^ 1, then L ^ 2); lane q then
+//    holds sample 4k + q of the quad's four channels and stores it as one dword (-1 % / -2 % on
+//    64x1000 / 64x480 against 2-byte pair stores, which were -5.6 % / -15 % against byte stores).
 template <class K>
 __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   wave_sync_lds();  // the previous block's A reads precede these stores
   if constexpr (K::P == 2) {
-    if (lane < 2 * K::C) {
-      int8_t* p = stg + 8 * K::SG * (lane & 1) + 2 * (lane >> 1);
+    static_assert(K::C % 2 == 0, "channel pairs");
+    const int c = lane >> 1;
+    const unsigned sel = (c & 1) ? 0x03020706u : 0x05040100u;
+    int8_t* p = stg + 8 * K::SG * (lane & 1) + 2 * (c & ~1) + K::SG * (c & 1);
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const unsigned w = (unsigned)raw[i >> 1];
-        *(unsigned short*)(p + K::SG * i) = (unsigned short)((i & 1) ? (w >> 16) : w);
-      }
+    for (int k = 0; k < 4; k++) {  // dword k: samples 4k .. 4k + 3 = time groups 2k, 2k + 1
+      const unsigned d = (unsigned)raw[k];
+      const unsigned w = __builtin_amdgcn_perm((unsigned)__builtin_amdgcn_mov_dpp((int)d, 0x4E, 0xF, 0xF, false), d, sel);
+      if (lane < 2 * K::C) *(unsigned*)(p + 2 * K::SG * k) = w;  // the even channel's lane: group 2k
     }
   } else {
-#ifdef MIB_CT_P1_B8
-    if (lane < K::C) {
-      int8_t* p = stg + lane;
-#pragma unroll
-      for (int i = 0; i < 16; i++) p[K::SG * i] = (int8_t)((unsigned)raw[i >> 2] >> (8 * (i & 3)));
-    }
-#else
-    // channel pairs (c, c ^ 1) trade dwords (DPP quad_perm [1,0,3,2]); one v_perm then forms the
-    // (channel c & ~1, c | 1) byte pairs of two samples: the even lane those of samples 4k, 4k + 2,
-    // the odd lane 4k + 1, 4k + 3.  Eight 2-byte stores per lane instead of sixteen byte stores.
-    static_assert(K::C % 2 == 0, "channel pairs");
-    const unsigned sel = (lane & 1) ? 0x03070105u : 0x06020400u;
-    int8_t* p = stg + (lane & ~1) + K::SG * (lane & 1);
+    static_assert(K::C % 4 == 0, "channel quads");
+    const unsigned sel1 = (lane & 1) ? 0x03070105u : 0x06020400u;
+    const unsigned sel2 = (lane & 2) ? 0x03020706u : 0x05040100u;
+    int8_t* p = stg + (lane & ~3) + K::SG * (lane & 3);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const unsigned d = (unsigned)raw[k];
-      const unsigned q = (unsigned)__builtin_amdgcn_mov_dpp((int)d, 0xB1, 0xF, 0xF, false);
-      const unsigned w = __builtin_amdgcn_perm(q, d, sel);
-      if (lane < K::C) {
-        *(unsigned short*)(p + K::SG * 4 * k) = (unsigned short)w;
-        *(unsigned short*)(p + K::SG * (4 * k + 2)) = (unsigned short)(w >> 16);
-      }
+      const unsigned a = __builtin_amdgcn_perm((unsigned)__builtin_amdgcn_mov_dpp((int)d, 0xB1, 0xF, 0xF, false), d, sel1);
+      const unsigned w = __builtin_amdgcn_perm((unsigned)__builtin_amdgcn_mov_dpp((int)a, 0x4E, 0xF, 0xF, false), a, sel2);
+      if (lane < K::C) *(unsigned*)(p + 4 * K::SG * k) = w;
     }
-#endif
   }
   wave_sync_lds();
-  return *(const v4i*)(stg + K::SG * (lane & 15) + 16 * (lane >> 4));
+  return staged_a<K>(stg, lane);
 }
 
 template <class K>
@@ -600,36 +593,25 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
 #pragma unroll
   for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
-  // channel-major: block i + 1 is staged (stores and A read, buffer (i + 1) & 1) before block i's
-  // MFMAs, so the staging latency passes under them
-  int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::NSTG * K::STG;
-  auto staged = [&](int i) -> v4i {
-    v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
-    if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
-#ifndef MIB_DIAG_CT_NOSTAGE
-    a = stage_block<K>(a, stg + (i % K::NSTG) * K::STG, lane);
-#endif
-    return a;
+  auto slot = [&](int i) -> v4i { return (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0]; };
+  auto compute = [&](v4i a, int i) {
+    const int blk = l1_blk<K>(wave, i);
+    if (blk == K::NB1 - 1) {  // the trial's last block: samples >= T are masked
+      l1_block<K, true>(a, blk, smem_y1, R, lane);
+    } else {
+      l1_block<K, false>(a, blk, smem_y1, R, lane);
+    }
   };
-  v4i an = {0, 0, 0, 0};
-  if constexpr (K::CT)
-    if (n > 0) an = staged(0);
+  int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;  // channel-major staging
 #pragma unroll
   for (int i = 0; i < K::NBW; i++) {
     if (i < n) {  // wave-uniform
-      const int blk = l1_blk<K>(wave, i);
-      v4i a;
+      v4i a = slot(i);
       if constexpr (K::CT) {
-        a = an;
-        if (i + 1 < n) an = staged(i + 1 < K::NBW ? i + 1 : 0);
-      } else {
-        a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
+        if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
+        a = stage_block<K>(a, stg, lane);
       }
-      if (blk == K::NB1 - 1) {  // the trial's last block: samples >= T are masked
-        l1_block<K, true>(a, blk, smem_y1, R, lane);
-      } else {
-        l1_block<K, false>(a, blk, smem_y1, R, lane);
-      }
+      compute(a, i);
     }
   }
   prefetch_l1<K>(rnext, R);
