@@ -84,7 +84,6 @@ struct SmallParams {
 // Operand fragments and requantisation constants, built by the host from the net.h arrays.
 struct DevParams {
   v4i l1_wfrag[2][64];      // layer-1 B operand per N-tile and lane
-  v4i l1_wfrag_ct[2][64];   // the same for the channel-major staging's window order (Cfg::SG)
   int l1_cinit[2][16];      // offset + FMAGIC_I per N-tile column
   float l1_r[2][16];        // reciprocal per N-tile column
   float l1_c[2][16];        // -(1.5 * 2^23) * r, exact
@@ -101,6 +100,7 @@ struct DevParams {
   // K-slots = the two filters' 96-slot bands side by side (K block diagonal, see forward_wg.hpp)
   v4i l2t_afrag[F2 / 2][3][64];
   SmallParams sp;
+  v4i l1_wfrag_ct[2][64];   // layer-1 B operand for the channel-major staging's window order (Cfg::SG)
 };
 
 // LO: lower clip bound, -128 (the C's __CLIP_R(x, 127), clip_balanced=False) or -127

@@ -593,25 +593,21 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
 #pragma unroll
   for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
-  auto slot = [&](int i) -> v4i { return (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0]; };
-  auto compute = [&](v4i a, int i) {
-    const int blk = l1_blk<K>(wave, i);
-    if (blk == K::NB1 - 1) {  // the trial's last block: samples >= T are masked
-      l1_block<K, true>(a, blk, smem_y1, R, lane);
-    } else {
-      l1_block<K, false>(a, blk, smem_y1, R, lane);
-    }
-  };
   int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;  // channel-major staging
 #pragma unroll
   for (int i = 0; i < K::NBW; i++) {
     if (i < n) {  // wave-uniform
-      v4i a = slot(i);
+      const int blk = l1_blk<K>(wave, i);
+      v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
       if constexpr (K::CT) {
-        if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
+        if (last_trial && blk == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
         a = stage_block<K>(a, stg, lane);
       }
-      compute(a, i);
+      if (blk == K::NB1 - 1) {  // the trial's last block: samples >= T are masked
+        l1_block<K, true>(a, blk, smem_y1, R, lane);
+      } else {
+        l1_block<K, false>(a, blk, smem_y1, R, lane);
+      }
     }
   }
   prefetch_l1<K>(rnext, R);

@@ -40,8 +40,8 @@ def main():
         L.net_trial_stride.restype = ctypes.c_size_t
         L.net_model_compute_batch_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                                     ctypes.c_int, ctypes.c_void_p]
-        L.net_model_compute_batch_ct.argtypes = L.net_model_compute_batch_async.argtypes
         if a.ct:
+            L.net_model_compute_batch_ct.argtypes = L.net_model_compute_batch_async.argtypes
             L.net_model_compute_batch_async = L.net_model_compute_batch_ct
         rc = L.net_params_load(blob, len(blob))
         assert rc == 0, (p, rc)
