@@ -10,7 +10,9 @@
  *       x.bin: n trials in the reference single-trial layout [T][C_ALIGN] int8; want.bin: the
  *       expected logits [n][N] int8.  Runs every trial through net_model_compute (host
  *       buffers), then all n at once through net_model_compute_batch (device buffers, packed
- *       [n][trial_stride] layout), and compares both with want.bin.  Exit 0 when all match.
+ *       [n][trial_stride] layout) and through net_model_compute_batch_ct (channel-major
+ *       [n][C][T], at an odd device address), and compares each with want.bin.  Exit 0 when all
+ *       match.
  *   net_host bench <params.blob> [B=65536] [steps=50]
  *       Times `steps` back-to-back net_model_compute_batch_async launches over B resident
  *       random trials with HIP events and prints one line of trials/s.
@@ -109,6 +111,28 @@ static int check(const char* blob, const char* xpath, const char* wpath, long n)
     long badb = 0;
     for (long b = 0; b < n; b++) badb += memcmp(y + (size_t)b * N, want + (size_t)b * N, (size_t)N) != 0;
     printf("net_model_compute_batch: %ld of %ld trials differ\n", badb, n);
+    /* channel-major [n][C][T] (input.npz's layout) straight into net_model_compute_batch_ct,
+       one byte into its allocation (the entry point takes any alignment) */
+    int8_t* cm = malloc((size_t)n * C * T);
+    for (long b = 0; b < n; b++)
+        for (int c = 0; c < C; c++)
+            for (int t = 0; t < T; t++) cm[((size_t)b * C + c) * T + t] = x[((size_t)b * T + t) * CA + c];
+    int8_t* dxc = NULL;
+    HIP_OK(hipMalloc((void**)&dxc, (size_t)n * C * T + 1));
+    HIP_OK(hipMemcpy(dxc + 1, cm, (size_t)n * C * T, hipMemcpyHostToDevice));
+    HIP_OK(hipMemset(dy, 0, (size_t)n * N));
+    rc = net_model_compute_batch_ct(dxc + 1, dy, (size_t)n, 0, NULL);
+    if (rc) {
+        fprintf(stderr, "net_model_compute_batch_ct: %s\n", net_error_string(rc));
+        return 1;
+    }
+    HIP_OK(hipMemcpy(y, dy, (size_t)n * N, hipMemcpyDeviceToHost));  /* null stream: after the launch */
+    long badc = 0;
+    for (long b = 0; b < n; b++) badc += memcmp(y + (size_t)b * N, want + (size_t)b * N, (size_t)N) != 0;
+    printf("net_model_compute_batch_ct: %ld of %ld trials differ\n", badc, n);
+    badb += badc;
+    hipFree(dxc);
+    free(cm);
     hipFree(dx);
     hipFree(dy);
     free(y);

@@ -45,6 +45,7 @@ def test_c_host_check(gpu, net_host, tmp_path, C, T, rb):
                         str(tmp_path / "want.bin"), str(n)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ok" in r.stdout
+    assert f"net_model_compute_batch_ct: 0 of {n} trials differ" in r.stdout
     # a wrong expectation is reported as a failure
     bad = want.copy()
     bad[3, 0] ^= 1
