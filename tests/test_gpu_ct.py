@@ -106,3 +106,43 @@ def test_ct_errors(gpu):
     assert L.net_model_compute_batch_ct(x.data_ptr(), y.data_ptr(), 0, 0, None) == lib.NET_OK
     with pytest.raises(ValueError):
         lib.forward_ct_torch(torch.zeros((2, 1125, 22), dtype=torch.int8, device="cuda"))
+
+
+def test_ct_graph_and_streams(gpu):
+    """The channel-major entry inside a captured HIP graph (channel-major forward -> class,
+    replayed over new inputs), and two launches racing on two streams (each equals the oracle)."""
+    import torch
+
+    ps = ParamSet.synthetic(seed=61)
+    lib.params_load(ps)
+    co = oracle.COracle(ps)
+    B, C, T = 777, 22, 1125
+    rng = np.random.default_rng(61)
+    xs = [rng.integers(-128, 128, size=(B, C, T)).astype(np.int8) for _ in range(3)]
+    xin = torch.from_numpy(xs[0]).cuda()
+    lib.forward_ct_torch(xin)  # eager call: uploads the parameters
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            logits = lib.forward_ct_torch(xin, stream=s)
+            cls = lib.argmax_torch(logits, stream=s)
+    for x in xs:
+        xin.copy_(torch.from_numpy(x))
+        g.replay()
+        torch.cuda.synchronize()
+        want = co.batch(_packed(torch, torch.from_numpy(x).cuda()).cpu().numpy(), nthreads=8)
+        assert np.array_equal(logits.cpu().numpy(), want)
+        assert np.array_equal(cls.cpu().numpy(), np.argmax(want, axis=1))
+    # two streams at once, different batches
+    a, b = torch.from_numpy(xs[1]).cuda(), torch.from_numpy(xs[2][:500]).cuda()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        ya = lib.forward_ct_torch(a, stream=s1)
+    with torch.cuda.stream(s2):
+        yb = lib.forward_ct_torch(b, stream=s2)
+    torch.cuda.synchronize()
+    assert np.array_equal(ya.cpu().numpy(), co.batch(_packed(torch, a).cpu().numpy(), nthreads=8))
+    assert np.array_equal(yb.cpu().numpy(), co.batch(_packed(torch, b).cpu().numpy(), nthreads=8))
