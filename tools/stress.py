@@ -9,7 +9,10 @@ outputs that differ from the expected ones.
      launch maps different trials to different workgroups and prefetch slots, and is compared
      with the oracle's logits permuted the same way.
 
-    python tools/stress.py [--lib path] [--n1 2000] [--n2 200] [--nb 8] [--B 65536]
+    python tools/stress.py [--lib path] [--n1 2000] [--n2 200] [--nb 8] [--B 65536] [--layout ct]
+
+  --layout ct stresses net_model_compute_batch_ct instead: the batches are channel-major
+  [B][C][T] (the oracle gets the same trials transposed).
 """
 import argparse
 import os
@@ -33,6 +36,7 @@ def main():
     ap.add_argument("--n2", type=int, default=200)
     ap.add_argument("--B", type=int, default=65536)
     ap.add_argument("--nb", type=int, default=8, help="distinct input batches per parameter mode")
+    ap.add_argument("--layout", default="tc", choices=("tc", "ct"))
     ap.add_argument("--variants", default="canonical",
                     help="comma list of build variants to stress: canonical, plain_bn, clip_balanced")
     a = ap.parse_args()
@@ -63,12 +67,20 @@ def main():
         g = torch.Generator(device="cuda:0").manual_seed(11 + stress)
         xs, wants = [], []
         t0 = time.time()
+        C, T = ps.dims.C, ps.dims.T
         for k in range(a.nb):
-            x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0", generator=g)
-            x[:, 22 * 1125:] = 0
-            xs.append(x)
+            if a.layout == "ct":
+                xc = torch.randint(-128, 128, (a.B, C * T), dtype=torch.int8, device="cuda:0", generator=g)
+                x = torch.zeros((a.B, stride), dtype=torch.int8, device="cuda:0")
+                x[:, : C * T] = xc.view(a.B, C, T).transpose(1, 2).reshape(a.B, C * T)
+                xs.append(xc)
+            else:
+                x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0", generator=g)
+                x[:, C * T:] = 0
+                xs.append(x)
             want = oracle.COracle(ps).batch(x.cpu().numpy(), nthreads=min(16, os.cpu_count() or 1))
             wants.append(torch.from_numpy(want).to("cuda:0"))
+            del x
         print(f"oracle on {a.nb} x {a.B} trials: {time.time() - t0:.1f} s", flush=True)
         xp = torch.empty_like(xs[0])
         y = torch.empty((a.B, 4), dtype=torch.int8, device="cuda:0")
@@ -79,7 +91,11 @@ def main():
             perm = torch.randperm(a.B, device="cuda:0", generator=g)
             torch.index_select(xs[k], 0, perm, out=xp)
             y.fill_(0x55)
-            lib.model_compute_batch(xp.data_ptr(), y.data_ptr(), a.B)
+            if a.layout == "ct":
+                rc = lib.load().net_model_compute_batch_ct(xp.data_ptr(), y.data_ptr(), a.B, 0, None)
+                assert rc == 0, rc
+            else:
+                lib.model_compute_batch(xp.data_ptr(), y.data_ptr(), a.B)
             torch.cuda.synchronize()
             bad = (y != wants[k][perm]).any(dim=1)
             nb = int(bad.sum())
@@ -88,7 +104,7 @@ def main():
                 if bad2 <= 5:
                     rows = torch.nonzero(bad).flatten()[:4].tolist()
                     print(f"batch launch {i}: {nb} trials differ, first {rows}", flush=True)
-        print(f"batch ({variant}, stress={stress}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
+        print(f"batch ({a.layout}, {variant}, stress={stress}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
               f"{a.nb * a.B} distinct ({time.time() - t0:.1f} s)", flush=True)
 
 if __name__ == "__main__":
