@@ -103,7 +103,14 @@ struct Cfg {
   static constexpr int NT4 = (8 * T64 + 63) / 64;       // L4 MFMAs of 64 time samples
   static constexpr L1Split SPL = l1_split(NB1);
   static constexpr int NBW = cmax(SPL.cm + (SPL.rm ? 1 : 0), SPL.cl);  // L1 blocks per wave (max)
-  static constexpr int PF = cmin(NBW, PF_MAX);          // of which prefetched a trial ahead
+#ifndef MIB_PF_MAX_PLAIN
+#define MIB_PF_MAX_PLAIN 3  // plain BN: fewer prefetched blocks, no spills (config B -5.4 %, C -13.6 %)
+#endif
+#ifndef MIB_PF_MAX_PLAIN_CT
+#define MIB_PF_MAX_PLAIN_CT 2
+#endif
+  // of which prefetched a trial ahead (the plain-BN builds hold more per-filter state)
+  static constexpr int PF = cmin(NBW, RB ? PF_MAX : CT_ ? MIB_PF_MAX_PLAIN_CT : MIB_PF_MAX_PLAIN);
   static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
   // full L2 tiles per filter, then a tail of TB blocks on the 16x16x64 chain when the wave's two
   // filters' tail columns fit its 16 columns (FPW * TC <= 16); otherwise (short trials, e.g.
