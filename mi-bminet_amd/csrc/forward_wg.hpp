@@ -31,6 +31,9 @@
 //   layer5  F2*T64 -> 4 linear + bias + requant: one wave, 16 lanes per class, DPP row
 //           reduction, one dword store.              (reference: layer5.c:43-89)
 // The plain (non-REORDER_BN) build requantises every layer-2/4 element in the floor form (l2n_out).
+// Channel-major input (Cfg::CT, net_model_compute_batch_ct): each layer-1 block is read as
+// 16-sample row segments, transposed through a per-wave LDS staging area (stage_block) and read
+// back as the MFMA A fragment; everything after that is the same code.
 #pragma once
 #include "forward_common.hpp"
 
