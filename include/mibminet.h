@@ -125,6 +125,11 @@ int net_model_compute_batch_ct(const int8_t* x, int8_t* y, size_t B, int device,
 int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y,
                                   const size_t* B, void* const* streams);
 
+/* The same split over channel-major shards: x[i] is [B[i]][C][T] int8 on devices[i] (as
+ * net_model_compute_batch_ct takes it). */
+int net_model_compute_batch_multi_ct(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y,
+                                     const size_t* B, void* const* streams);
+
 /* Input quantiser / transposer (the step before the path; reference
  * edge-eegnet_wolf/data/gen_input_header.py:66-76 with python_utils/functional.py:308-334):
  * x: DEVICE pointer to B float trials [B][C][T]; y: DEVICE pointer to the batched int8 layout

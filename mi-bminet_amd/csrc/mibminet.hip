@@ -912,8 +912,9 @@ int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int de
   return argmax_batch(logits, cls, B, N, device, stream);
 }
 
-int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y,
-                                  const size_t* B, void* const* streams) {
+namespace {
+int batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y, const size_t* B,
+                void* const* streams, bool ct) {
   if (ndev < 1 || ndev > MAX_DEVICES || !devices || !x || !y || !B) return NET_ERR_INVALID;
   // enqueue every shard first (launches are asynchronous), then wait: one host thread keeps all
   // devices busy at once.  On an error the shards already enqueued are waited for before
@@ -929,7 +930,7 @@ int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* co
     return first;
   };
   for (int i = 0; i < ndev; i++) {
-    const int rc = net_model_compute_batch_async(x[i], y[i], B[i], devices[i], streams ? streams[i] : nullptr);
+    const int rc = batch_async(x[i], y[i], B[i], devices[i], streams ? streams[i] : nullptr, ct);
     if (rc) {
       (void)wait(i);
       return rc;
@@ -937,6 +938,17 @@ int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* co
   }
   if (streams) return NET_OK;
   return wait(ndev);
+}
+}  // namespace
+
+int net_model_compute_batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y,
+                                  const size_t* B, void* const* streams) {
+  return batch_multi(ndev, devices, x, y, B, streams, false);
+}
+
+int net_model_compute_batch_multi_ct(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y,
+                                     const size_t* B, void* const* streams) {
+  return batch_multi(ndev, devices, x, y, B, streams, true);
 }
 
 int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device) {

@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
     "net_pack_trials_i8", "net_model_compute_batch_multi", "net_model_compute_batch_ct",
+    "net_model_compute_batch_multi_ct",
 )
 
 
@@ -104,6 +105,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_argmax_batch.restype = i
     L.net_model_compute_batch_ct.argtypes = [vp, vp, sz, i, vp]
     L.net_model_compute_batch_ct.restype = i
+    L.net_model_compute_batch_multi_ct.argtypes = [i, vp, vp, vp, vp, vp]
+    L.net_model_compute_batch_multi_ct.restype = i
     _lib = L
     return L
 
@@ -320,9 +323,10 @@ def pack_trials_torch(x, stream=None):
     return y
 
 
-def model_compute_batch_multi(xs, ys, devices) -> None:
-    """net_model_compute_batch_multi: xs[i] / ys[i] are device tensors on devices[i]
-    ([B_i][trial_stride] and [B_i][N] int8); one host call runs every shard and waits for all."""
+def model_compute_batch_multi(xs, ys, devices, channel_major: bool = False) -> None:
+    """net_model_compute_batch_multi(_ct): xs[i] / ys[i] are device tensors on devices[i]
+    ([B_i][trial_stride], or [B_i][C][T] with ``channel_major``, and [B_i][N] int8); one host call
+    runs every shard and waits for all."""
     n = len(devices)
     if not (len(xs) == len(ys) == n):
         raise ValueError("xs, ys and devices must have the same length")
@@ -330,4 +334,5 @@ def model_compute_batch_multi(xs, ys, devices) -> None:
     xp = (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])
     yp = (ctypes.c_void_p * n)(*[y.data_ptr() for y in ys])
     bs = (ctypes.c_size_t * n)(*[x.shape[0] for x in xs])
-    _check(load().net_model_compute_batch_multi(n, dev, xp, yp, bs, None), "net_model_compute_batch_multi")
+    fn = load().net_model_compute_batch_multi_ct if channel_major else load().net_model_compute_batch_multi
+    _check(fn(n, dev, xp, yp, bs, None), "net_model_compute_batch_multi")

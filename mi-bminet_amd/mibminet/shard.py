@@ -71,11 +71,12 @@ def gather_logits(y_shard: np.ndarray, batch: int, world: int, n_out: int = 4) -
     return np.concatenate(parts, axis=0)
 
 
-def forward_devices(x_global, devices):
-    """Logits of the whole batch ``x_global`` ([B][trial_stride] int8, host array or tensor) split
-    over ``devices`` with ``shard_bounds``: each shard is copied to its device, every device runs
-    concurrently from this one host thread (net_model_compute_batch_multi), and the [B][N] logits
-    come back concatenated in trial order."""
+def forward_devices(x_global, devices, channel_major: bool = False):
+    """Logits of the whole batch ``x_global`` ([B][trial_stride] int8, or [B][C][T] with
+    ``channel_major``; host array or tensor) split over ``devices`` with ``shard_bounds``: each
+    shard is copied to its device, every device runs concurrently from this one host thread
+    (net_model_compute_batch_multi / _multi_ct), and the [B][N] logits come back concatenated in
+    trial order."""
     import torch
     from . import lib
 
@@ -91,5 +92,5 @@ def forward_devices(x_global, devices):
         ys.append(torch.empty((hi - lo, n_out), dtype=torch.int8, device=dev))
     for d in set(devices):
         torch.cuda.synchronize(d)  # the copies above ran on torch's streams
-    lib.model_compute_batch_multi(xs, ys, list(devices))
+    lib.model_compute_batch_multi(xs, ys, list(devices), channel_major=channel_major)
     return np.concatenate([y.cpu().numpy() for y in ys], axis=0)

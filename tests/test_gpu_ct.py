@@ -146,3 +146,22 @@ def test_ct_graph_and_streams(gpu):
     torch.cuda.synchronize()
     assert np.array_equal(ya.cpu().numpy(), co.batch(_packed(torch, a).cpu().numpy(), nthreads=8))
     assert np.array_equal(yb.cpu().numpy(), co.batch(_packed(torch, b).cpu().numpy(), nthreads=8))
+
+
+def test_ct_static_split(gpu):
+    """Config E's static split over channel-major shards (net_model_compute_batch_multi_ct, device 0
+    listed 4 times): equal to one channel-major launch over the whole batch and to the oracle at
+    every shard boundary."""
+    import torch
+    from mibminet.shard import forward_devices, shard_bounds
+
+    ps = ParamSet.synthetic(seed=71)
+    lib.params_load(ps)
+    B, C, T, world = 4099, 22, 1125, 4
+    x = _ct_batch(torch, B, C, T, seed=71)
+    y_split = forward_devices(x, [0] * world, channel_major=True)
+    y_one = lib.forward_ct_torch(x).cpu().numpy()
+    assert np.array_equal(y_split, y_one)
+    edges = sorted({i for r in range(world) for lo, hi in [shard_bounds(B, world, r)] for i in (lo, hi - 1)})
+    want = oracle.COracle(ps).batch(_packed(torch, x[edges]).cpu().numpy(), nthreads=8)
+    np.testing.assert_array_equal(y_split[edges], want)
