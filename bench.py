@@ -272,7 +272,7 @@ def main():
         dist.all_gather_object(per_rank, mine)
         elapsed = elapsed_max
 
-    info = lib.launch_info(B, local)
+    info = lib.launch_info(B, local, channel_major=a.layout == "ct")
     if rank == 0:
         # N > 1: the slowest rank's kernel average (each rank's is listed under "ranks")
         avg_kernel_s = (max(r["kernel_ms"] for r in per_rank) if per_rank else rank_avg_ms) / 1e3

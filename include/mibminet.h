@@ -163,6 +163,8 @@ int net_set_device(int device);
 /* Kernel launch geometry used for a batch of B trials (for profiling/roofline bookkeeping):
  * out[0] = grid size (workgroups), out[1] = threads per workgroup, out[2] = LDS bytes. */
 int net_launch_info(size_t B, int device, int32_t* out);
+/* The same for the channel-major kernel (net_model_compute_batch_ct). */
+int net_launch_info_ct(size_t B, int device, int32_t* out);
 
 const char* net_error_string(int code);
 int net_version(void);

@@ -959,7 +959,8 @@ int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device) {
   return hip_err(hipStreamSynchronize(nullptr));
 }
 
-int net_launch_info(size_t B, int device, int32_t* out) {
+namespace {
+int launch_info(size_t B, int device, int32_t* out, bool ct) {
   if (!out || device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
@@ -971,8 +972,13 @@ int net_launch_info(size_t B, int device, int32_t* out) {
   if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
-  return launch_forward(v, ds, nullptr, nullptr, nullptr, B, nullptr, out);
+  return launch_forward(v, ds, nullptr, nullptr, nullptr, B, nullptr, out, ct);
 }
+}  // namespace
+
+int net_launch_info(size_t B, int device, int32_t* out) { return launch_info(B, device, out, false); }
+
+int net_launch_info_ct(size_t B, int device, int32_t* out) { return launch_info(B, device, out, true); }
 
 int net_forward(const int8_t* p_data, int8_t* p_output) { return run_single(0, p_data, p_output); }
 

@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
     "net_pack_trials_i8", "net_model_compute_batch_multi", "net_model_compute_batch_ct",
-    "net_model_compute_batch_multi_ct",
+    "net_model_compute_batch_multi_ct", "net_launch_info_ct",
 )
 
 
@@ -89,6 +89,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_set_device.restype = i
     L.net_launch_info.argtypes = [sz, i, vp]
     L.net_launch_info.restype = i
+    L.net_launch_info_ct.argtypes = [sz, i, vp]
+    L.net_launch_info_ct.restype = i
     L.net_error_string.argtypes = [i]
     L.net_error_string.restype = ctypes.c_char_p
     L.net_version.argtypes = []
@@ -233,9 +235,10 @@ def model_compute_batch(x_ptr: int, y_ptr: int, B: int, device: int = 0, stream:
         _check(L.net_model_compute_batch_async(x_ptr, y_ptr, B, device, stream), "net_model_compute_batch_async")
 
 
-def launch_info(B: int, device: int = 0) -> dict:
+def launch_info(B: int, device: int = 0, channel_major: bool = False) -> dict:
     arr = (ctypes.c_int32 * 3)()
-    _check(load().net_launch_info(B, device, arr), "net_launch_info")
+    fn = load().net_launch_info_ct if channel_major else load().net_launch_info
+    _check(fn(B, device, arr), "net_launch_info")
     return {"grid": arr[0], "threads": arr[1], "lds_bytes": arr[2]}
 
 
