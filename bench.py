@@ -49,9 +49,10 @@ def parse():
     ap.add_argument("--variant", default="canonical", choices=("canonical", "plain_bn", "clip_balanced"),
                     help="build variant the parameter blob selects: the canonical -DREORDER_BN build, the "
                          "plain-BN branches (layer2.c:139-210, layer4.c:91-133) or golden-model balanced clipping")
-    ap.add_argument("--layout", default="tc", choices=("tc", "ct"),
+    ap.add_argument("--layout", default="tc", choices=("tc", "ct", "f32"),
                     help="input layout: tc = time-major batched trials [B][stride] (net_model_compute_batch), "
-                         "ct = channel-major [B][C][T] (net_model_compute_batch_ct, transposed inside the kernel)")
+                         "ct = channel-major [B][C][T] (net_model_compute_batch_ct, transposed inside the kernel), "
+                         "f32 = float32 EEG [B][C][T] (net_model_compute_batch_f32, quantised inside the kernel)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed launches before the warmup steps (GPU clock ramp)")
@@ -202,7 +203,13 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(a.seed * 1000 + rank)
     C, T = cfg["C"], cfg["T"]
-    if a.layout == "ct":
+    if a.layout == "f32":
+        # float EEG whose quantised values spread over the int8 range (scale = 3 sigma)
+        xf = torch.randn((B, C, T), dtype=torch.float32, device=dev, generator=g)
+        qscale = 3.0
+        x = lib.quantize_input_torch(xf, qscale)  # the same trials as int8, time-major (CPU baseline)
+        torch.cuda.synchronize(dev)
+    elif a.layout == "ct":
         xc = torch.randint(-128, 128, (B, C, T), dtype=torch.int8, device=dev, generator=g)
         x = torch.zeros((B, stride), dtype=torch.int8, device=dev)  # the same trials, time-major
         x[:, : C * T] = xc.transpose(1, 2).reshape(B, C * T)         # (CPU baseline and --pcie)
@@ -213,9 +220,14 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
     ct_fn = lib.load().net_model_compute_batch_ct
+    f32_fn = lib.load().net_model_compute_batch_f32
 
     def step():
-        if a.layout == "ct":
+        if a.layout == "f32":
+            rc = f32_fn(xf.data_ptr(), y.data_ptr(), B, qscale, local, sp)
+            if rc:
+                raise lib.NetError(rc, "net_model_compute_batch_f32")
+        elif a.layout == "ct":
             rc = ct_fn(xc.data_ptr(), y.data_ptr(), B, local, sp)
             if rc:
                 raise lib.NetError(rc, "net_model_compute_batch_ct")
@@ -272,11 +284,11 @@ def main():
         dist.all_gather_object(per_rank, mine)
         elapsed = elapsed_max
 
-    info = lib.launch_info(B, local, channel_major=a.layout == "ct")
+    info = lib.launch_info(B, local, channel_major=a.layout != "tc")
     if rank == 0:
         # N > 1: the slowest rank's kernel average (each rank's is listed under "ranks")
         avg_kernel_s = (max(r["kernel_ms"] for r in per_rank) if per_rank else rank_avg_ms) / 1e3
-        alg_bytes_trial = cfg["C"] * cfg["T"] + 4
+        alg_bytes_trial = cfg["C"] * cfg["T"] * (4 if a.layout == "f32" else 1) + 4
         achieved = alg_bytes_trial * B / avg_kernel_s / 1e9
         traffic = None
         try:
@@ -292,7 +304,8 @@ def main():
         out = {
             "metric": (METRIC if a.config == "b22" and a.variant == "canonical" and a.layout == "tc"
                        else f"EEG trials/sec ({cfg['name']}, {a.variant} build, "
-                            f"{'channel-major' if a.layout == 'ct' else 'time-major'} input) at batch {B}"),
+                            f"{ {'ct': 'channel-major', 'f32': 'float32 channel-major', 'tc': 'time-major'}[a.layout]} "
+                            f"input) at batch {B}"),
             "value": value,
             "unit": "trials/s",
             "n_gpus": world,
@@ -306,15 +319,17 @@ def main():
             "dtype": "int8",
             "data": "synthetic (uniform int8 EEG generated on device; seeded synthetic integer weights)",
             "config": {"workload": cfg["name"], "variant": a.variant, "C": cfg["C"], "T": cfg["T"], "batch_per_gpu": B,
-                       "input_layout": ("[B][C][T] channel-major (net_model_compute_batch_ct)" if a.layout == "ct"
-                                        else "[B][T][C] time-major, 16-byte trial stride (net_model_compute_batch)"),
+                       "input_layout": {"ct": "[B][C][T] channel-major (net_model_compute_batch_ct)",
+                                        "f32": "[B][C][T] float32, quantised in the kernel (net_model_compute_batch_f32)",
+                                        "tc": "[B][T][C] time-major, 16-byte trial stride (net_model_compute_batch)"}[a.layout],
                        "global_batch": world * B, "weight_bits": cfg["wbits"],
                        "parallelism": f"dp{world} static batch split, no collectives",
                        "grid": info["grid"], "threads": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d>>" % (cfg["C"], cfg["T"], a.variant != "plain_bn",
-                                                                                a.variant == "clip_balanced", a.layout == "ct"),
+                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d,FQ=%d>>" % (
+                             cfg["C"], cfg["T"], a.variant != "plain_bn", a.variant == "clip_balanced",
+                             a.layout != "tc", a.layout == "f32"),
                          "avg_kernel_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes_trial * B},
             "cpu_baseline": None,

@@ -116,6 +116,16 @@ int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int devi
  * the kernel (no separate pack pass).  Enqueued on `stream` (NULL = null stream), no host sync. */
 int net_model_compute_batch_ct(const int8_t* x, int8_t* y, size_t B, int device, void* stream);
 
+/* Float EEG straight into the forward: x: DEVICE pointer to B float32 trials [B][C][T] (the
+ * reference's input.npz, 4-byte aligned), y: DEVICE pointer [B][N].  Each layer-1 block is
+ * quantised in the kernel exactly as net_quantize_input_f32 does it (x / scale, clip to [-1, 1],
+ * * 127, truncate, in float32; gen_input_header.py:66-76), then staged as in
+ * net_model_compute_batch_ct: no int8 copy of the batch in memory.  scale = absMaxValue of quant1,
+ * in [2^-60, 2^60] (NET_ERR_RANGE otherwise: the in-kernel quotient is exact there; use
+ * net_quantize_input_f32 + net_model_compute_batch_async beyond).  Enqueued on `stream` (NULL =
+ * null stream), no host sync. */
+int net_model_compute_batch_f32(const float* x, int8_t* y, size_t B, float scale, int device, void* stream);
+
 /* Several devices from one host thread (static split, no collectives): shard i is
  * x[i] / y[i] / B[i] on devices[i] (DEVICE pointers of that device).  Every shard is enqueued
  * before any is waited for, so the devices run concurrently.  streams == NULL: each device's null

@@ -27,6 +27,10 @@ int mibminet_test_reciprocal(int32_t fac, int64_t vmax, int32_t kmax, int32_t ma
  * Returns 0 with mbits (the magic the MFMA C-init adds to the offset), r and c, or NET_ERR_RANGE. */
 int mibminet_test_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* mbits, float* r, float* c);
 
+/* The float32 input quantiser of net_model_compute_batch_f32 (in-kernel, Markstein-corrected
+ * quotient) on a flat device array: q[i] = quantize(x[i]) for i < n.  Enqueued on `stream`. */
+int mibminet_test_quantize_f32(const float* x, int8_t* q, size_t n, float scale, int device, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -92,9 +92,11 @@ constexpr L1Split l1_split(int nb1) {
   return best;
 }
 
-template <int C_, int T_, bool RB_ = true, bool CB_ = false, bool CT_ = false>
+template <int C_, int T_, bool RB_ = true, bool CB_ = false, bool CT_ = false, bool FQ_ = false>
 struct Cfg {
   static constexpr int C = C_, T = T_;
+  static constexpr bool FQ = FQ_;                       // float32 channel-major trials, quantised in layer1
+  static_assert(!FQ_ || CT_, "float input is channel-major");
   static constexpr bool RB = RB_;                       // -DREORDER_BN variant (canonical)
   static constexpr bool CB = CB_;                       // golden-model clip_balanced: clip to [-127, 127]
   static constexpr bool CT = CT_;                       // channel-major [C][T] trials, staged in LDS (layer1)
@@ -113,7 +115,8 @@ struct Cfg {
 #define MIB_PF_MAX_PLAIN_CT 2
 #endif
   // of which prefetched a trial ahead (the plain-BN builds hold more per-filter state)
-  static constexpr int PF = cmin(NBW, RB ? PF_MAX : CT_ ? MIB_PF_MAX_PLAIN_CT : MIB_PF_MAX_PLAIN);
+  // (float input: the first block's four 16-byte pieces; the others load one block ahead)
+  static constexpr int PF = FQ_ ? 4 : cmin(NBW, RB ? PF_MAX : CT_ ? MIB_PF_MAX_PLAIN_CT : MIB_PF_MAX_PLAIN);
   static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
   // full L2 tiles per filter, then a tail of TB blocks on the 16x16x64 chain when the wave's two
   // filters' tail columns fit its 16 columns (FPW * TC <= 16); otherwise (short trials, e.g.
@@ -131,7 +134,7 @@ struct Cfg {
   static constexpr int Y1ROW = P * PLANE;
   // batched trial stride (bytes): time-major trials are padded to 16 bytes, channel-major ones
   // are the caller's contiguous [B][C][T]
-  static constexpr int XTRIAL = CT ? C * T : align16(T * C);
+  static constexpr int XTRIAL = FQ ? 4 * C * T : CT ? C * T : align16(T * C);
   // channel-major staging (layer1, CT): one layer-1 block per wave, time group j at SG j.  P == 2:
   // window slot 2c + p = channel c of the group's sample p (44 bytes for C = 22); P == 1: slot c.
   // The last group's window runs 16 bytes past the block (zero weights meet them).
@@ -317,7 +320,8 @@ struct Regs {
   float r2[FPW];
   v4i a31, a32;            // layer-3 tile-1 / tile-2 band fragments of the wave's filter pair
   float r3, c3;            // layer-3 requant constants (uniform)
-  v4i pf[K::PF];           // layer-1 fragments prefetched one trial ahead
+  float qs, qy;            // float input's quantisation scale and RN(1 / scale) (K::FQ)
+  v4i pf[K::PF > 0 ? K::PF : 1];  // layer-1 fragments prefetched one trial ahead
   int xoff;                // lane_xoff(lane)
 };
 
@@ -366,7 +370,8 @@ __device__ __forceinline__ Rsrc trial_rsrc(const int8_t* xt, int trials_left, in
     // a dword straddling num_records reads as zeros.  So the view runs 3 bytes past the trial,
     // into the next trial's bytes, except for the batch's last trial, whose straddling dword is
     // completed by byte loads (ct_tail).
-    const int n = trials_left <= 0 ? 0 : trials_left == 1 ? K::C * K::T : K::C * K::T + 3;
+    // (float input: dword-aligned rows, so the view is exactly the trial)
+    const int n = trials_left <= 0 ? 0 : (trials_left == 1 || K::FQ) ? K::XTRIAL : K::XTRIAL + 3;
     return __builtin_amdgcn_make_buffer_rsrc((void*)xt, (short)0, n, 0x00020000);
   }
   const int wb = l1_start<K>(wave) * 16 * K::GS;  // byte offset of the wave's first block
@@ -382,7 +387,7 @@ __device__ __forceinline__ int lane_xoff(int lane, int wave) {
     // slot i adds 16 P i samples.  Lanes past the rows read zeros without a fetch.
     const int c = K::P == 2 ? lane >> 1 : lane, h = K::P == 2 ? lane & 1 : 0;
     if (c >= K::C) return (int)0x80000000u;
-    return c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h;
+    return (K::FQ ? 4 : 1) * (c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h);
   }
 #ifndef MIB_NO_ZERO_PAD_LANES
   // A lane whose 16-byte chunk lies wholly past the group's P * C bytes (C = 22: bytes 48..63)
@@ -484,12 +489,23 @@ __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   return staged_a<K>(stg, lane);
 }
 
+// float input (K::FQ): 16-byte piece m of the lane's 64 bytes of block slot i
+template <class K>
+__device__ __forceinline__ v4i load_f(Rsrc r, int xoff, int i, int m) {
+  return (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xoff + 64 * K::P * i + 16 * m, 0, 0);
+}
+
 template <class K>
 __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R) {
   // laundered: otherwise xoff + 16 GS i is hoisted out of the trial loop into a register per slot
   // instead of riding in the loads' immediate offsets
   int xo = R.xoff;
   asm volatile("" : "+v"(xo));
+  if constexpr (K::FQ) {  // the first block's four pieces
+#pragma unroll
+    for (int m = 0; m < 4; m++) R.pf[m] = load_f<K>(r, xo, 0, m);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, i);
 }
@@ -595,9 +611,71 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
 
 // Layer 1: x[T][C] (HBM, via R.pf) -> y1 rows (LDS, position 32 + t).  Prefetches the next
 // trial's fragments (rnext) into R.pf once the current ones are consumed.
+// Float input (K::FQ): 4 float32 samples (raw bits) -> 4 int8 bytes, the reference's input
+// quantisation (gen_input_header.py:66-76, functional.py:308-334: x / s, clip to [-1, 1], * 254 / 2,
+// truncate; each step rounded in float32), the same function as quant::quantize_one<float>.  The
+// correctly rounded quotient RN(x / s) comes from Markstein's correction instead of the division
+// sequence: q0 = RN(x y) with y = RN(1 / s) (host), r = x - q0 s exactly (fma), RN(q0 + r y) =
+// RN(x / s) (y within half an ulp of 1 / s and q0 within one ulp of x / s).  x is first clamped to
+// [-2s, 2s], which keeps q0 finite and changes no output (|x| > s clips to +-1 either way); NaN
+// clamps to -2s (fmaxf), as in the two-pass quantiser.  Checked against that quantiser on every
+// float32 bit pattern for several scales (tests/test_gpu_f32.py).
+__device__ __forceinline__ int quantize1(float x, float s, float y) {
+  x = fminf(fmaxf(x, -2.0f * s), 2.0f * s);  // (fmed3 would take NaN to +2s: measured)
+  const float q0 = x * y;
+  const float r = __builtin_fmaf(-q0, s, x);
+  float q = __builtin_fmaf(r, y, q0);
+  q = __builtin_amdgcn_fmed3f(q, -1.0f, 1.0f);
+  return (int)(q * 127.0f);
+}
+
+__device__ __forceinline__ unsigned quantize4(v4i f, float s, float y) {
+  unsigned w = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) w |= ((unsigned)quantize1(__int_as_float(f[j]), s, y) & 255u) << (8 * j);
+  return w;
+}
+
+// test hook (mibminet_test_quantize_f32): the in-kernel quantiser on a flat array
+__global__ void k_quantize_flat(const float* __restrict__ x, int8_t* __restrict__ q, long long n, float s, float y) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    q[i] = (int8_t)quantize1(x[i], s, y);
+}
+
 template <class K>
 __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, Regs<K>& R, int wave, int lane,
                                        bool last_trial = false) {
+  if constexpr (K::FQ) {
+    // float32 rows: the lane's 16 samples of a block are 64 bytes (4 loads), quantised to the
+    // 16 int8 bytes the channel-major staging takes.  Block 0 was loaded during the previous
+    // trial (R.pf); block i + 1 is loaded while block i is quantised and computed.
+    const int n = l1_count<K>(wave);
+    int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;
+    v4i cur[4] = {R.pf[0], R.pf[1], R.pf[2], R.pf[3]};
+#pragma unroll
+    for (int i = 0; i < K::NBW; i++) {
+      if (i < n) {  // wave-uniform
+        const int blk = l1_blk<K>(wave, i);
+        v4i nxt[4] = {cur[0], cur[1], cur[2], cur[3]};
+        if (i + 1 < n)
+#pragma unroll
+          for (int m = 0; m < 4; m++) nxt[m] = load_f<K>(rcur, R.xoff, i + 1, m);
+        v4i raw;
+#pragma unroll
+        for (int m = 0; m < 4; m++) raw[m] = (int)quantize4(cur[m], R.qs, R.qy);
+        const v4i a = stage_block<K>(raw, stg, lane);
+        if (blk == K::NB1 - 1) {
+          l1_block<K, true>(a, blk, smem_y1, R, lane);
+        } else {
+          l1_block<K, false>(a, blk, smem_y1, R, lane);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; m++) cur[m] = nxt[m];
+      }
+    }
+    prefetch_l1<K>(rnext, R);
+    return;
+  }
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
   v4i xa[NX > 0 ? NX : 1];
 #pragma unroll
@@ -976,12 +1054,15 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
 // Fused forward over a batch (persistent, grid-strided over trials).
 template <class K>
 __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void k_forward(
-    const DevParams* __restrict__ prm, const int8_t* __restrict__ x, int8_t* __restrict__ out, int B) {
+    const DevParams* __restrict__ prm, const int8_t* __restrict__ x, int8_t* __restrict__ out, int B, float qs,
+    float qy) {
   __shared__ __attribute__((aligned(16))) int8_t smem[K::LDS];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   Regs<K> R;
   setup<K>(prm, smem, R, tid, wave, lane);
+  R.qs = qs;
+  R.qy = qy;
   const SmallParams* sp = (const SmallParams*)(smem + K::OFF_SP);
   if ((int)blockIdx.x < B)
     prefetch_l1<K>(trial_rsrc<K>(x + MIB_TRIAL_OFF(blockIdx.x), MIB_TRIALS_LEFT(blockIdx.x), wave), R);

@@ -468,19 +468,20 @@ Variant variant_of(const HostParams& hp) {
   return v;
 }
 
-template <int C, int T, bool CT, class F>
+template <int C, int T, bool CT, bool FQ, class F>
 int with_variant(const Variant& v, F&& f) {
-  if (v.rb) return v.cb ? f(wg::Cfg<C, T, true, true, CT>{}) : f(wg::Cfg<C, T, true, false, CT>{});
-  return v.cb ? f(wg::Cfg<C, T, false, true, CT>{}) : f(wg::Cfg<C, T, false, false, CT>{});
+  if (v.rb) return v.cb ? f(wg::Cfg<C, T, true, true, CT, FQ>{}) : f(wg::Cfg<C, T, true, false, CT, FQ>{});
+  return v.cb ? f(wg::Cfg<C, T, false, true, CT, FQ>{}) : f(wg::Cfg<C, T, false, false, CT, FQ>{});
 }
 
-// Calls f(K{}) with the kernel configuration K of the variant (CT: channel-major input trials).
-template <bool CT = false, class F>
+// Calls f(K{}) with the kernel configuration K of the variant (CT: channel-major input trials;
+// FQ: float32 channel-major trials quantised in the kernel).
+template <bool CT = false, bool FQ = false, class F>
 int dispatch(const Variant& v, F&& f) {
   switch (v.shape) {
-    case 0: return with_variant<22, 1125, CT>(v, f);
-    case 1: return with_variant<64, 1000, CT>(v, f);
-    case 2: return with_variant<64, 480, CT>(v, f);
+    case 0: return with_variant<22, 1125, CT, FQ>(v, f);
+    case 1: return with_variant<64, 1000, CT, FQ>(v, f);
+    case 2: return with_variant<64, 480, CT, FQ>(v, f);
     default: return NET_ERR_UNSUPPORTED;
   }
 }
@@ -635,7 +636,7 @@ int ensure_scratch(DeviceState& ds, size_t bytes) {
 // Persistent grid: as many resident workgroups as the occupancy allows (two per CU).
 template <class K>
 int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y, size_t B,
-                     hipStream_t st, int32_t* info) {
+                     hipStream_t st, int32_t* info, float qs = 0.0f) {
   static std::atomic<int> bpc{0};  // per kernel instantiation (LDS and registers differ)
   int blocks_per_cu = bpc.load();
   if (blocks_per_cu == 0) {
@@ -648,14 +649,17 @@ int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_
   const int grid = (int)(B < cap ? B : cap);
   if (info) { info[0] = grid; info[1] = wg::NTHREADS; info[2] = K::LDS; return NET_OK; }
   if (B == 0) return NET_OK;
-  hipLaunchKernelGGL(wg::k_forward<K>, dim3(grid), dim3(wg::NTHREADS), 0, st, p, x, y, (int)B);
+  const float qy = qs > 0.0f ? 1.0f / qs : 0.0f;  // RN(1 / scale): IEEE division on the host
+  hipLaunchKernelGGL(wg::k_forward<K>, dim3(grid), dim3(wg::NTHREADS), 0, st, p, x, y, (int)B, qs, qy);
   return hip_err(hipGetLastError());
 }
 
+// layout: 0 time-major int8, 1 channel-major int8, 2 channel-major float32 (scale qs)
 int launch_forward(const Variant& v, DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y,
-                   size_t B, hipStream_t st, int32_t* info = nullptr, bool ct = false) {
-  auto f = [&](auto k) { return launch_forward_t<decltype(k)>(ds, p, x, y, B, st, info); };
-  return ct ? dispatch<true>(v, f) : dispatch<false>(v, f);
+                   size_t B, hipStream_t st, int32_t* info = nullptr, int layout = 0, float qs = 0.0f) {
+  auto f = [&](auto k) { return launch_forward_t<decltype(k)>(ds, p, x, y, B, st, info, qs); };
+  if (layout == 2) return dispatch<true, true>(v, f);
+  return layout == 1 ? dispatch<true, false>(v, f) : dispatch<false, false>(v, f);
 }
 
 int launch_layer(const Variant& v, const DevParams* p, const int8_t* in, int8_t* out, int stage, hipStream_t st) {
@@ -859,9 +863,16 @@ int net_set_device(int device) {
 namespace {
 // ct: channel-major trials [B][C][T] (any alignment, trial stride C T bytes); otherwise the
 // time-major batched layout (16-byte aligned, stride net_trial_stride())
-int batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream, bool ct) {
+// layout: 0 time-major int8, 1 channel-major int8, 2 channel-major float32 (scale qs)
+int batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream, int layout, float qs = 0.0f) {
   if ((!x || !y) && B) return NET_ERR_INVALID;
-  if ((!ct && ((uintptr_t)x & 15) != 0) || ((uintptr_t)y & 3) != 0) return NET_ERR_INVALID;
+  const uintptr_t xa = layout == 0 ? 15 : layout == 2 ? 3 : 0;
+  if (((uintptr_t)x & xa) != 0 || ((uintptr_t)y & 3) != 0) return NET_ERR_INVALID;
+  if (layout == 2 && !(qs > 0.0f && qs <= 3.4e38f)) return NET_ERR_INVALID;
+  // the in-kernel quotient correction stays exact while its products are normal floats: scales in
+  // [2^-60, 2^60] (checked on every float32 input, tests/test_gpu_f32.py); others: the two-pass
+  // quantiser (net_quantize_input_f32), which divides
+  if (layout == 2 && !(qs >= 0x1p-60f && qs <= 0x1p60f)) return NET_ERR_RANGE;
   if (device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
@@ -874,16 +885,20 @@ int batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream, 
   if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
-  return launch_forward(v, ds, ds.cur, x, y, B, (hipStream_t)stream, nullptr, ct);
+  return launch_forward(v, ds, ds.cur, x, y, B, (hipStream_t)stream, nullptr, layout, qs);
 }
 }  // namespace
 
 int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream) {
-  return batch_async(x, y, B, device, stream, false);
+  return batch_async(x, y, B, device, stream, 0);
 }
 
 int net_model_compute_batch_ct(const int8_t* x, int8_t* y, size_t B, int device, void* stream) {
-  return batch_async(x, y, B, device, stream, true);
+  return batch_async(x, y, B, device, stream, 1);
+}
+
+int net_model_compute_batch_f32(const float* x, int8_t* y, size_t B, float scale, int device, void* stream) {
+  return batch_async((const int8_t*)x, y, B, device, stream, 2, scale);
 }
 
 int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, float scale, int device, void* stream) {
@@ -901,6 +916,19 @@ int net_pack_trials_i8(const int8_t* x, int8_t* y, size_t B, int C, int T, int d
 int mibminet_test_reciprocal(int32_t fac, int64_t vmax, int32_t kmax, int32_t magic, float* r, float* c) {
   if (!r || (magic && !c) || vmax < 0 || vmax >= (1 << 24)) return NET_ERR_INVALID;
   return choose_reciprocal(fac, r, magic ? c : nullptr, kmax, vmax) ? NET_OK : NET_ERR_RANGE;
+}
+
+int mibminet_test_quantize_f32(const float* x, int8_t* q, size_t n, float scale, int device, void* stream) {
+  if ((!x || !q) && n) return NET_ERR_INVALID;
+  if (!(scale > 0.0f && scale <= 3.4e38f)) return NET_ERR_INVALID;
+  if (!(scale >= 0x1p-60f && scale <= 0x1p60f)) return NET_ERR_RANGE;
+  if (const int rc = check_device(device)) return rc;
+  if (n == 0) return NET_OK;
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
+  hipLaunchKernelGGL(wg::k_quantize_flat, dim3(4096), dim3(256), 0, (hipStream_t)stream, x, q, (long long)n, scale,
+                     1.0f / scale);
+  return hip_err(hipGetLastError());
 }
 
 int mibminet_test_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* mbits, float* r, float* c) {
@@ -930,7 +958,7 @@ int batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* co
     return first;
   };
   for (int i = 0; i < ndev; i++) {
-    const int rc = batch_async(x[i], y[i], B[i], devices[i], streams ? streams[i] : nullptr, ct);
+    const int rc = batch_async(x[i], y[i], B[i], devices[i], streams ? streams[i] : nullptr, ct ? 1 : 0);
     if (rc) {
       (void)wait(i);
       return rc;

@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "net_model_compute_batch_async", "net_set_device", "net_launch_info", "net_error_string",
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
     "net_pack_trials_i8", "net_model_compute_batch_multi", "net_model_compute_batch_ct",
-    "net_model_compute_batch_multi_ct", "net_launch_info_ct",
+    "net_model_compute_batch_multi_ct", "net_launch_info_ct", "net_model_compute_batch_f32",
 )
 
 
@@ -91,6 +91,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_launch_info.restype = i
     L.net_launch_info_ct.argtypes = [sz, i, vp]
     L.net_launch_info_ct.restype = i
+    L.net_model_compute_batch_f32.argtypes = [vp, vp, sz, ctypes.c_float, i, vp]
+    L.net_model_compute_batch_f32.restype = i
     L.net_error_string.argtypes = [i]
     L.net_error_string.restype = ctypes.c_char_p
     L.net_version.argtypes = []
@@ -274,6 +276,22 @@ def forward_ct_torch(x, stream=None):
     s = torch.cuda.current_stream(x.device) if stream is None else stream
     _check(load().net_model_compute_batch_ct(x.data_ptr(), y.data_ptr(), B, x.device.index or 0, s.cuda_stream),
            "net_model_compute_batch_ct")
+    return y
+
+
+def forward_f32_torch(x, scale: float, stream=None):
+    """net_model_compute_batch_f32: x is a CUDA/HIP float32 tensor [B][C][T] (float EEG, the
+    reference's input.npz layout) -> logits [B][N], quantised inside the fused kernel."""
+    import torch
+
+    d = _dims()
+    if x.dtype != torch.float32 or not x.is_cuda or not x.is_contiguous() or tuple(x.shape[1:]) != (d.C, d.T):
+        raise ValueError(f"x must be a contiguous float32 device tensor [B][{d.C}][{d.T}]")
+    B = x.shape[0]
+    y = torch.empty((B, d.N), dtype=torch.int8, device=x.device)
+    s = torch.cuda.current_stream(x.device) if stream is None else stream
+    _check(load().net_model_compute_batch_f32(x.data_ptr(), y.data_ptr(), B, scale, x.device.index or 0,
+                                              s.cuda_stream), "net_model_compute_batch_f32")
     return y
 
 
