@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variant", default="canonical", choices=("canonical", "plain_bn", "clip_balanced"))
     ap.add_argument("--ct", action="store_true", help="channel-major input (net_model_compute_batch_ct)")
+    ap.add_argument("--f32", action="store_true", help="float32 channel-major input (net_model_compute_batch_f32)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     C, T = {"b22": (22, 1125), "c64": (64, 1000), "p64": (64, 480)}[a.cfg]
@@ -43,11 +44,19 @@ def main():
         if a.ct:
             L.net_model_compute_batch_ct.argtypes = L.net_model_compute_batch_async.argtypes
             L.net_model_compute_batch_async = L.net_model_compute_batch_ct
+        if a.f32:  # same call shape, the scale bound in (3 sigma of the standard-normal input)
+            f = L.net_model_compute_batch_f32
+            f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_float, ctypes.c_int,
+                          ctypes.c_void_p]
+            L.net_model_compute_batch_async = (lambda f: lambda x, y, B, d, s: f(x, y, B, 3.0, d, s))(f)
         rc = L.net_params_load(blob, len(blob))
         assert rc == 0, (p, rc)
         libs.append(L)
     stride = C * T if a.ct else libs[0].net_trial_stride()
-    x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0")
+    if a.f32:
+        x = torch.randn((a.B, C, T), dtype=torch.float32, device="cuda:0")
+    else:
+        x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0")
     y = torch.empty((a.B, 4), dtype=torch.int8, device="cuda:0")
     st = torch.cuda.current_stream()
     outs = []
