@@ -12,7 +12,9 @@ outputs that differ from the expected ones.
     python tools/stress.py [--lib path] [--n1 2000] [--n2 200] [--nb 8] [--B 65536] [--layout ct]
 
   --layout ct stresses net_model_compute_batch_ct instead: the batches are channel-major
-  [B][C][T] (the oracle gets the same trials transposed).
+  [B][C][T] (the oracle gets the same trials transposed).  --layout f32 stresses
+  net_model_compute_batch_f32 on float32 batches against the two-pass GPU chain
+  (net_quantize_input_f32 + the time-major forward, which the GPU tests pin to the oracle).
 """
 import argparse
 import os
@@ -36,7 +38,7 @@ def main():
     ap.add_argument("--n2", type=int, default=200)
     ap.add_argument("--B", type=int, default=65536)
     ap.add_argument("--nb", type=int, default=8, help="distinct input batches per parameter mode")
-    ap.add_argument("--layout", default="tc", choices=("tc", "ct"))
+    ap.add_argument("--layout", default="tc", choices=("tc", "ct", "f32"))
     ap.add_argument("--variants", default="canonical",
                     help="comma list of build variants to stress: canonical, plain_bn, clip_balanced")
     a = ap.parse_args()
@@ -69,6 +71,11 @@ def main():
         t0 = time.time()
         C, T = ps.dims.C, ps.dims.T
         for k in range(a.nb):
+            if a.layout == "f32":
+                xf = torch.randn((a.B, C, T), dtype=torch.float32, device="cuda:0", generator=g)
+                xs.append(xf.view(a.B, C * T))
+                wants.append(lib.forward_torch(lib.quantize_input_torch(xf, 3.0)).clone())
+                continue
             if a.layout == "ct":
                 xc = torch.randint(-128, 128, (a.B, C * T), dtype=torch.int8, device="cuda:0", generator=g)
                 x = torch.zeros((a.B, stride), dtype=torch.int8, device="cuda:0")
@@ -91,7 +98,10 @@ def main():
             perm = torch.randperm(a.B, device="cuda:0", generator=g)
             torch.index_select(xs[k], 0, perm, out=xp)
             y.fill_(0x55)
-            if a.layout == "ct":
+            if a.layout == "f32":
+                rc = lib.load().net_model_compute_batch_f32(xp.data_ptr(), y.data_ptr(), a.B, 3.0, 0, None)
+                assert rc == 0, rc
+            elif a.layout == "ct":
                 rc = lib.load().net_model_compute_batch_ct(xp.data_ptr(), y.data_ptr(), a.B, 0, None)
                 assert rc == 0, rc
             else:
