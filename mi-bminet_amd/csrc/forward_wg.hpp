@@ -617,23 +617,50 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
 // correctly rounded quotient RN(x / s) comes from Markstein's correction instead of the division
 // sequence: q0 = RN(x y) with y = RN(1 / s) (host), r = x - q0 s exactly (fma), RN(q0 + r y) =
 // RN(x / s) (y within half an ulp of 1 / s and q0 within one ulp of x / s).  x is first clamped to
-// [-2s, 2s], which keeps q0 finite and changes no output (|x| > s clips to +-1 either way); NaN
-// clamps to -2s (fmaxf), as in the two-pass quantiser.  Checked against that quantiser on every
-// float32 bit pattern for several scales (tests/test_gpu_f32.py).
-__device__ __forceinline__ int quantize1(float x, float s, float y) {
-  x = fminf(fmaxf(x, -2.0f * s), 2.0f * s);  // (fmed3 would take NaN to +2s: measured)
+// [-s, s]: RN is monotone, so RN(x / s) then lies in [-1, 1] and the reference's clip has nothing
+// left to do (|x| > s gives RN(x / s) beyond +-1 and clips to +-1; the clamped x = +-s gives exactly
+// +-1).  NaN clamps to -s (fmaxf), as in the two-pass quantiser.  q * 127 is then within
+// [-127, 127], so its truncation needs no saturation and goes straight into its byte of the packed
+// word (SDWA byte destination).  Checked against the two-pass quantiser on every float32 bit
+// pattern for several scales (tests/test_gpu_f32.py).
+__device__ __forceinline__ float quantize1_f(float x, float s, float y) {
+#ifdef MIB_FQ_OLD  // round-3 form (clamp to [-2s, 2s], clip after the quotient), for same-box A/B
+  x = fminf(fmaxf(x, -2.0f * s), 2.0f * s);
   const float q0 = x * y;
   const float r = __builtin_fmaf(-q0, s, x);
-  float q = __builtin_fmaf(r, y, q0);
-  q = __builtin_amdgcn_fmed3f(q, -1.0f, 1.0f);
-  return (int)(q * 127.0f);
+  return __builtin_amdgcn_fmed3f(__builtin_fmaf(r, y, q0), -1.0f, 1.0f) * 127.0f;
+#else
+  x = fminf(fmaxf(x, -s), s);
+  const float q0 = x * y;
+  const float r = __builtin_fmaf(-q0, s, x);
+  return __builtin_fmaf(r, y, q0) * 127.0f;
+#endif
+}
+
+__device__ __forceinline__ int quantize1(float x, float s, float y) {
+  return (int)quantize1_f(x, s, y);  // trunc toward zero
 }
 
 __device__ __forceinline__ unsigned quantize4(v4i f, float s, float y) {
+#ifdef MIB_FQ_OLD
   unsigned w = 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) w |= ((unsigned)quantize1(__int_as_float(f[j]), s, y) & 255u) << (8 * j);
   return w;
+#else
+  // v_cvt_i32_f32 truncates toward zero; the byte destination keeps the low 8 bits (the int8 value,
+  // as |q * 127| <= 127) and leaves the word's other bytes as they are
+  unsigned w;
+  asm("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD"
+      : "=v"(w) : "v"(quantize1_f(__int_as_float(f[0]), s, y)));
+  asm("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+      : "+v"(w) : "v"(quantize1_f(__int_as_float(f[1]), s, y)));
+  asm("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+      : "+v"(w) : "v"(quantize1_f(__int_as_float(f[2]), s, y)));
+  asm("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
+      : "+v"(w) : "v"(quantize1_f(__int_as_float(f[3]), s, y)));
+  return w;
+#endif
 }
 
 // test hook (mibminet_test_quantize_f32): the in-kernel quantiser on a flat array
