@@ -295,8 +295,10 @@ def main():
             # HBM bytes per launch measured by PMC counters for this config and batch
             # (tools/collect_profile.py), per config under "configs"
             tj = json.load(open(a.traffic_json))
-            tc = tj.get("configs", {}).get(a.config, tj if tj.get("config") == a.config else {})
-            if tc.get("batch") == B and a.variant == "canonical" and a.layout == "tc":
+            # (time-major under the config's key, other input layouts under "<config>_<layout>")
+            key = a.config if a.layout == "tc" else f"{a.config}_{a.layout}"
+            tc = tj.get("configs", {}).get(key, tj if tj.get("config") == key else {})
+            if tc.get("batch") == B and a.variant == "canonical":
                 traffic = tc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
