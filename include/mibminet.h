@@ -146,7 +146,7 @@ int net_model_compute_batch_multi_ct(int ndev, const int* devices, const int8_t*
  * ([B][stride], stride = C*T rounded up to 16, each trial [T][C], pad bytes zero), computed as
  * trunc(clip(x / scale, -1, 1) * 127) in the input's precision.  scale = absMaxValue of the
  * network's quant1 activation.  Enqueued on `stream` (NULL = null stream), no host sync.
- * Any B up to INT32_MAX in one call (batches past 65,535 trials loop inside the kernel).  y must be
+ * Any B up to INT32_MAX - 65,535 in one call (batches past 65,535 trials loop inside the kernel).  y must be
  * 16-byte aligned (as net_model_compute_batch requires of its input) and one trial's input must
  * stay below 2 GiB (C * T * sizeof(element) < 2^31); NET_ERR_INVALID otherwise. */
 int net_quantize_input_f32(const float* x, int8_t* y, size_t B, int C, int T, float scale, int device,
@@ -157,13 +157,14 @@ int net_quantize_input_f64(const double* x, int8_t* y, size_t B, int C, int T, d
 /* The step after the path: cls[b] = index of the largest of the N int8 logits of trial b, the
  * first one on ties (torch.max(pr_outs, dim=1) of the reference's accuracy meter,
  * QuantLab/quantlab/BCI-CompIV-2a/edgeEEGNet/postprocess.py:6-8).  logits: DEVICE pointer [B][N]
- * (as net_model_compute_batch writes it), cls: DEVICE pointer [B].  1 <= N <= 64.  Enqueued on
+ * (as net_model_compute_batch writes it), cls: DEVICE pointer [B].  1 <= N <= 64,
+ * B <= INT32_MAX - 1024 (NET_ERR_INVALID otherwise).  Enqueued on
  * `stream` (NULL = null stream), no host sync. */
 int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int device, void* stream);
 
 /* Already-quantised int8 trials in channel-major [B][C][T] (the layout of the reference's
  * input.npz, transposed by gen_input_header.py:74 on the host): the same GPU transpose into the
- * batched [B][stride] layout, without the quantisation.  DEVICE pointers, B <= INT32_MAX,
+ * batched [B][stride] layout, without the quantisation.  DEVICE pointers, B <= INT32_MAX - 65,535,
  * C <= 64, y 16-byte aligned, enqueued on `stream`, no host sync. */
 int net_pack_trials_i8(const int8_t* x, int8_t* y, size_t B, int C, int T, int device, void* stream);
 

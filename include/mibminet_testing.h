@@ -31,6 +31,20 @@ int mibminet_test_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* m
  * quotient) on a flat device array: q[i] = quantize(x[i]) for i < n.  Enqueued on `stream`. */
 int mibminet_test_quantize_f32(const float* x, int8_t* q, size_t n, float scale, int device, void* stream);
 
+/* The multi-device driver of net_model_compute_batch_multi[_ct] run with recording stand-ins
+ * instead of device work (no device needed): writes the order of its steps into `log` as
+ * "P<device>" (parameter image made resident), "E<shard>" (shard enqueued) and "W<n>" (the first
+ * n shards waited for), with the enqueue of shard `fail_at` failing (-1: none).  Returns what the
+ * driver returns. */
+int mibminet_test_multi_order(int ndev, const int* devices, int fail_at, char* log, size_t len);
+
+/* Parameter-image uploads so far, and how many of them happened while the multi-device entry
+ * points were enqueueing shards (0 when every device is prepared before the first enqueue). */
+int mibminet_test_upload_stats(int64_t* uploads, int64_t* uploads_while_enqueueing);
+
+/* Number of parameter-image copies resident on `device`. */
+int mibminet_test_device_images(int device);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,23 @@ __device__ unsigned long long g_stamps[24];
 #define MIB_STAMP_FLUSH(cond, slot)
 #endif
 
+// Diagnostic in-kernel clock (tools/clock_probe.hip builds with -DMIB_CLOCK; compiled out
+// otherwise): one s_memtime / s_memrealtime pair around the trial loop per workgroup, summed
+// per workgroup over launches into g_clk[2 wg], g_clk[2 wg + 1].  No stamp inside the loop, and
+// nothing the kernel computes reads g_clk.  clock = d(memtime) / d(memrealtime) x 100 MHz.
+#ifdef MIB_CLOCK
+constexpr int CLK_SLOTS = 4096;
+__device__ unsigned long long g_clk[2 * CLK_SLOTS];
+#define MIB_CLOCK_INIT const unsigned long long _ck_t0 = __builtin_amdgcn_s_memtime(), \
+  _ck_r0 = __builtin_amdgcn_s_memrealtime();
+#define MIB_CLOCK_FLUSH if (threadIdx.x == 0 && blockIdx.x < CLK_SLOTS) { \
+  const unsigned long long _t = __builtin_amdgcn_s_memtime(), _r = __builtin_amdgcn_s_memrealtime(); \
+  atomicAdd(&g_clk[2 * blockIdx.x], _t - _ck_t0); atomicAdd(&g_clk[2 * blockIdx.x + 1], _r - _ck_r0); }
+#else
+#define MIB_CLOCK_INIT
+#define MIB_CLOCK_FLUSH
+#endif
+
 __host__ __device__ constexpr int align16(int x) { return (x + 15) & ~15; }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int cmin(int a, int b) { return a < b ? a : b; }

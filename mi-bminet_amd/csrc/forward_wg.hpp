@@ -663,10 +663,20 @@ __device__ __forceinline__ unsigned quantize4(v4i f, float s, float y) {
 #endif
 }
 
-// test hook (mibminet_test_quantize_f32): the in-kernel quantiser on a flat array
+// test hook (mibminet_test_quantize_f32): the in-kernel quantiser on a flat array, four elements
+// at a time through quantize4, the instruction sequence the forward kernel runs (elements past n
+// in the last group are quantised as 0.0f and not stored)
 __global__ void k_quantize_flat(const float* __restrict__ x, int8_t* __restrict__ q, long long n, float s, float y) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
-    q[i] = (int8_t)quantize1(x[i], s, y);
+  for (long long i = 4 * ((long long)blockIdx.x * blockDim.x + threadIdx.x); i < n;
+       i += 4 * (long long)gridDim.x * blockDim.x) {
+    v4i f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) f[j] = i + j < n ? __float_as_int(x[i + j]) : 0;
+    const unsigned w = quantize4(f, s, y);
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      if (i + j < n) q[i + j] = (int8_t)(w >> (8 * j));
+  }
 }
 
 template <class K>
@@ -1098,6 +1108,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   MIB_STAMP_INIT
+  MIB_CLOCK_INIT
   // Per trial two barriers: A after layer 1 (layer 2 of a filter reads all waves' layer-1
   // output), B after layer 3 (layer 4 reads all filters).  Layers 2 and 3 of a filter run on the
   // wave that owns it, with no barrier between.  After B the last wave runs layers 4 and 5 while
@@ -1176,6 +1187,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   }
   MIB_STAMP_FLUSH(tid == 0, 0)
   MIB_STAMP_FLUSH(tid == 64 * (NWAVES - 1), 1)
+  MIB_CLOCK_FLUSH
 }
 
 // Single-trial, single-layer kernel for the reference's per-layer entry points (debug/parity):

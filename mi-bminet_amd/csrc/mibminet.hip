@@ -17,6 +17,7 @@
 #include <memory>
 #include <atomic>
 #include <mutex>
+#include <string>
 #include <vector>
 
 #include "../../include/mibminet.h"
@@ -492,23 +493,30 @@ size_t trial_stride(const Dims& d) { return ((size_t)d.C * d.T + 15) / 16 * 16; 
 // One device copy of the parameter image per loaded generation: a load never overwrites a copy
 // that a kernel may still read, so launches in flight and launches captured into a HIP graph keep
 // the image (and with it the compiled variant) they were enqueued with.  A reload of a
-// byte-identical image reuses its copy.  The copies per device are bounded: when a new image would
-// make more than MAX_IMAGES, the device is synchronised (no launch still reads an old copy) and
-// the least recently used copies are freed; net_params_unload frees every copy the same way.  A
-// HIP graph that captured a launch with an evicted image must be re-captured.
+// byte-identical image reuses its copy.  When a new image would make more than MAX_IMAGES copies,
+// only copies that no launch can still read are freed, least recently used first: every batched
+// launch records an event per (copy, stream), and a copy is free once all its events have
+// completed.  A copy used by a launch under stream capture (a HIP graph may replay it at any
+// time) or on more than MAX_STREAMS streams is kept until net_params_unload.  Nothing here waits
+// for the device, so a load never stalls or breaks a caller's capture; if no copy can be freed
+// the device simply keeps more than MAX_IMAGES.  net_params_unload synchronises each device and
+// frees every copy (graphs that captured a launch must not be replayed after it).
 constexpr size_t MAX_IMAGES = 8;
+constexpr size_t MAX_STREAMS = 16;
 
 struct DevImage {
   std::shared_ptr<const DevParams> host;  // what was uploaded
   DevParams* dev = nullptr;
   uint64_t used = 0;                      // DeviceState::tick at the last selection
+  bool pinned = false;                    // captured into a graph (or too many streams): kept
+  std::vector<std::pair<hipStream_t, hipEvent_t>> last;  // the last launch per stream
 };
 
 struct DeviceState {
   std::mutex mu;
   uint64_t gen = 0;             // params generation of `cur`
   DevParams* cur = nullptr;     // device copy of that generation
-  std::vector<DevImage> images; // the copies uploaded to this device (at most MAX_IMAGES)
+  std::vector<DevImage> images; // the copies uploaded to this device
   uint64_t tick = 0;
   int8_t* d_in = nullptr;       // single-trial scratch
   int8_t* d_out = nullptr;
@@ -527,6 +535,10 @@ DeviceState g_devs[MAX_DEVICES];
 std::atomic<int> g_single_device{0};  // net_set_device (read by every single-trial call)
 std::atomic<int> g_device_count{-1};
 thread_local int t_last_error = NET_OK;
+// test counters (mibminet_test_upload_stats): parameter uploads, and those made while
+// batch_multi was enqueueing shards (must stay 0: every device is prepared first)
+std::atomic<long> g_uploads{0}, g_uploads_enqueue{0};
+thread_local bool t_enqueueing = false;
 
 inline int hip_err(hipError_t e) { return e == hipSuccess ? NET_OK : NET_ERR_HIP - (int)e; }
 
@@ -562,7 +574,70 @@ Snapshot snapshot() {
   return Snapshot{g_host, g_dev, g_gen};
 }
 
-// Ensure `dev` holds the current parameters (ds.cur); called with ds.mu held and the device current.
+void free_image(DevImage& im) {
+  for (auto& se : im.last) (void)hipEventDestroy(se.second);
+  im.last.clear();
+  (void)hipFree(im.dev);
+  im.dev = nullptr;
+}
+
+// no launch recorded on the copy can still be running (graph-captured copies never qualify)
+bool image_idle(const DevImage& im) {
+  if (im.pinned) return false;
+  for (const auto& se : im.last)
+    if (hipEventQuery(se.second) != hipSuccess) return false;
+  return true;
+}
+
+// Frees least-recently-used idle copies (never ds.cur) until fewer than MAX_IMAGES remain or none
+// is idle.  No device synchronisation.
+void evict_idle(DeviceState& ds) {
+  while (ds.images.size() >= MAX_IMAGES) {
+    int victim = -1;
+    for (int i = 0; i < (int)ds.images.size(); i++) {
+      const DevImage& im = ds.images[i];
+      if (im.dev == ds.cur || !image_idle(im)) continue;
+      if (victim < 0 || im.used < ds.images[victim].used) victim = i;
+    }
+    if (victim < 0) return;
+    free_image(ds.images[victim]);
+    ds.images.erase(ds.images.begin() + victim);
+  }
+}
+
+// After a batched launch with ds.cur on `st` (ds.mu held, device current): remember it, so that
+// the copy is freed only once the launch has finished.  Under stream capture the copy is pinned.
+void note_launch(DeviceState& ds, hipStream_t st) {
+  for (DevImage& im : ds.images) {
+    if (im.dev != ds.cur) continue;
+    if (im.pinned) return;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+      im.pinned = true;  // a graph may replay this launch at any time
+      return;
+    }
+    for (auto& se : im.last)
+      if (se.first == st) {
+        if (hipEventRecord(se.second, st) != hipSuccess) im.pinned = true;
+        return;
+      }
+    hipEvent_t ev = nullptr;
+    if (im.last.size() >= MAX_STREAMS || hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      im.pinned = true;
+      return;
+    }
+    if (hipEventRecord(ev, st) != hipSuccess) {
+      (void)hipEventDestroy(ev);
+      im.pinned = true;
+      return;
+    }
+    im.last.emplace_back(st, ev);
+    return;
+  }
+}
+
+// Ensure `dev` holds the parameters of snapshot s (ds.cur); called with ds.mu held and the device
+// current.
 int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
   if (!s.host) return NET_ERR_NO_PARAMS;
   if (ds.cus == 0) {
@@ -579,29 +654,21 @@ int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
         im.used = ++ds.tick;
         return NET_OK;
       }
-    if (ds.images.size() >= MAX_IMAGES) {
-      // evict the least recently used copies once every launch on the device has finished
-      hipError_t e = hipDeviceSynchronize();
-      if (e != hipSuccess) return hip_err(e);
-      std::sort(ds.images.begin(), ds.images.end(),
-                [](const DevImage& a, const DevImage& b) { return a.used > b.used; });
-      while (ds.images.size() >= MAX_IMAGES) {
-        (void)hipFree(ds.images.back().dev);
-        ds.images.pop_back();
-      }
-    }
+    evict_idle(ds);
     DevImage im;
     im.host = s.dev;
     im.used = ++ds.tick;
     hipError_t e = hipMalloc((void**)&im.dev, sizeof(DevParams));
     if (e != hipSuccess) return hip_err(e);
     e = hipMemcpy(im.dev, s.dev.get(), sizeof(DevParams), hipMemcpyHostToDevice);
+    g_uploads++;
+    if (t_enqueueing) g_uploads_enqueue++;
     if (e != hipSuccess) {
       (void)hipFree(im.dev);
       return hip_err(e);
     }
-    ds.images.push_back(im);
-    ds.cur = im.dev;
+    ds.images.push_back(std::move(im));
+    ds.cur = ds.images.back().dev;
     ds.gen = s.gen;
   }
   return NET_OK;
@@ -746,7 +813,8 @@ template <class F>
 int quantize_input(const F* x, int8_t* y, size_t B, int C, int T, F scale, int device, void* stream) {
   if ((!x || !y) && B) return NET_ERR_INVALID;
   if (C < 1 || C > quant::CMAX || T < 1 || device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
-  if (B > (size_t)INT32_MAX || !(scale > 0)) return NET_ERR_INVALID;
+  // trial indices are int in the kernel: b + gridDim.y (<= B + YMAX) must not wrap
+  if (B > (size_t)INT32_MAX - quant::YMAX || !(scale > 0)) return NET_ERR_INVALID;
   // one trial's input bytes form one buffer view (32-bit range); the tiles leave as 16-byte stores
   if ((size_t)C * T * sizeof(F) >= (size_t)1 << 31 || ((uintptr_t)y & 15)) return NET_ERR_INVALID;
   if (B == 0) return NET_OK;
@@ -765,7 +833,10 @@ int quantize_input(const F* x, int8_t* y, size_t B, int C, int T, F scale, int d
 
 int argmax_batch(const int8_t* logits, int32_t* out, size_t B, int N, int device, void* stream) {
   if ((!logits || !out) && B) return NET_ERR_INVALID;
-  if (N < 1 || N > cls::NMAX || device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
+  // trial indices are int in the kernels: 4 q + 3 and blockIdx.x * CTHREADS + threadIdx.x reach
+  // at most B + 4 CTHREADS, which must not wrap
+  if (N < 1 || N > cls::NMAX || device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX - 4 * cls::CTHREADS)
+    return NET_ERR_INVALID;
   if (B == 0) return NET_OK;
   if (const int rc = check_device(device)) return rc;
   DeviceGuard guard(device);
@@ -831,7 +902,7 @@ void net_params_unload(void) {
     if (ds.images.empty()) continue;
     DeviceGuard guard(d);
     if (guard.err != hipSuccess || hipDeviceSynchronize() != hipSuccess) continue;  // keep them
-    for (DevImage& im : ds.images) (void)hipFree(im.dev);
+    for (DevImage& im : ds.images) free_image(im);
     ds.images.clear();
     ds.cur = nullptr;
   }
@@ -861,10 +932,21 @@ int net_set_device(int device) {
 }
 
 namespace {
+// Makes sure `device` holds the parameter image of snapshot s (uploaded on first use).
+int prepare_device(int device, const Snapshot& s) {
+  if (const int rc = check_device(device)) return rc;
+  DeviceState& ds = g_devs[device];
+  std::lock_guard<std::mutex> lk(ds.mu);
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
+  return ensure_device(ds, device, s);
+}
+
 // ct: channel-major trials [B][C][T] (any alignment, trial stride C T bytes); otherwise the
 // time-major batched layout (16-byte aligned, stride net_trial_stride())
 // layout: 0 time-major int8, 1 channel-major int8, 2 channel-major float32 (scale qs)
-int batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream, int layout, float qs = 0.0f) {
+int batch_async_s(const Snapshot& s, const int8_t* x, int8_t* y, size_t B, int device, void* stream, int layout,
+                  float qs = 0.0f) {
   if ((!x || !y) && B) return NET_ERR_INVALID;
   const uintptr_t xa = layout == 0 ? 15 : layout == 2 ? 3 : 0;
   if (((uintptr_t)x & xa) != 0 || ((uintptr_t)y & 3) != 0) return NET_ERR_INVALID;
@@ -873,8 +955,8 @@ int batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream, 
   // [2^-60, 2^60] (checked on every float32 input, tests/test_gpu_f32.py); others: the two-pass
   // quantiser (net_quantize_input_f32), which divides
   if (layout == 2 && !(qs >= 0x1p-60f && qs <= 0x1p60f)) return NET_ERR_RANGE;
-  if (device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX) return NET_ERR_INVALID;
-  Snapshot s = snapshot();
+  // trial indices are int in the kernel: b + gridDim.x (grid <= 2 per CU) must not wrap
+  if (device < 0 || device >= MAX_DEVICES || B > (size_t)INT32_MAX - 65536) return NET_ERR_INVALID;
   if (!s.host) return NET_ERR_NO_PARAMS;
   const Variant v = variant_of(*s.host);
   if (!v.ok()) return NET_ERR_UNSUPPORTED;
@@ -885,8 +967,37 @@ int batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream, 
   if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
-  return launch_forward(v, ds, ds.cur, x, y, B, (hipStream_t)stream, nullptr, layout, qs);
+  rc = launch_forward(v, ds, ds.cur, x, y, B, (hipStream_t)stream, nullptr, layout, qs);
+  if (rc == NET_OK && B) note_launch(ds, (hipStream_t)stream);
+  return rc;
 }
+
+int batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream, int layout, float qs = 0.0f) {
+  return batch_async_s(snapshot(), x, y, B, device, stream, layout, qs);
+}
+
+// The multi-device driver: (1) every listed device gets the parameter image before any shard is
+// enqueued, so a first call uploads to all devices up front instead of starting them one after
+// another; (2) every shard is enqueued (asynchronous launches), then (3) waited for.  On an
+// enqueue error the shards already enqueued are waited for before returning.
+extern "C++" {
+template <class Prep, class Enq, class Wait>
+int multi_driver(int ndev, const int* devices, bool wait_all, Prep&& prep, Enq&& enq, Wait&& wait) {
+  for (int i = 0; i < ndev; i++) {
+    bool seen = false;
+    for (int j = 0; j < i; j++) seen = seen || devices[j] == devices[i];
+    if (seen) continue;
+    if (const int rc = prep(devices[i])) return rc;
+  }
+  for (int i = 0; i < ndev; i++) {
+    if (const int rc = enq(i)) {
+      (void)wait(i);
+      return rc;
+    }
+  }
+  return wait_all ? wait(ndev) : NET_OK;
+}
+}  // extern "C++"
 }  // namespace
 
 int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream) {
@@ -936,6 +1047,34 @@ int mibminet_test_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* m
   return choose_floor_form(fac, emax, vmax, mbits, r, c) ? NET_OK : NET_ERR_RANGE;
 }
 
+int mibminet_test_multi_order(int ndev, const int* devices, int fail_at, char* log, size_t len) {
+  if (!log || !len || ndev < 1 || ndev > MAX_DEVICES || !devices) return NET_ERR_INVALID;
+  std::string out;
+  auto prep = [&](int d) { out += "P" + std::to_string(d) + " "; return NET_OK; };
+  auto enq = [&](int i) {
+    out += "E" + std::to_string(i) + " ";
+    return i == fail_at ? NET_ERR_INVALID : NET_OK;
+  };
+  auto wait = [&](int n) { out += "W" + std::to_string(n) + " "; return NET_OK; };
+  const int rc = multi_driver(ndev, devices, true, prep, enq, wait);
+  std::snprintf(log, len, "%s", out.c_str());
+  return rc;
+}
+
+int mibminet_test_upload_stats(int64_t* uploads, int64_t* uploads_while_enqueueing) {
+  if (!uploads || !uploads_while_enqueueing) return NET_ERR_INVALID;
+  *uploads = g_uploads.load();
+  *uploads_while_enqueueing = g_uploads_enqueue.load();
+  return NET_OK;
+}
+
+int mibminet_test_device_images(int device) {
+  if (device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
+  DeviceState& ds = g_devs[device];
+  std::lock_guard<std::mutex> lk(ds.mu);
+  return (int)ds.images.size();
+}
+
 int net_argmax_batch(const int8_t* logits, int32_t* cls, size_t B, int N, int device, void* stream) {
   return argmax_batch(logits, cls, B, N, device, stream);
 }
@@ -944,9 +1083,9 @@ namespace {
 int batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* const* y, const size_t* B,
                 void* const* streams, bool ct) {
   if (ndev < 1 || ndev > MAX_DEVICES || !devices || !x || !y || !B) return NET_ERR_INVALID;
-  // enqueue every shard first (launches are asynchronous), then wait: one host thread keeps all
-  // devices busy at once.  On an error the shards already enqueued are waited for before
-  // returning, so no kernel still writes a caller's buffer when the error reaches it.
+  // one parameter snapshot for every shard (a concurrent net_params_load cannot split the batch)
+  const Snapshot s = snapshot();
+  if (!s.host) return NET_ERR_NO_PARAMS;
   auto wait = [&](int n) -> int {
     int first = NET_OK;
     for (int i = 0; i < n; i++) {
@@ -957,15 +1096,13 @@ int batch_multi(int ndev, const int* devices, const int8_t* const* x, int8_t* co
     }
     return first;
   };
-  for (int i = 0; i < ndev; i++) {
-    const int rc = batch_async(x[i], y[i], B[i], devices[i], streams ? streams[i] : nullptr, ct ? 1 : 0);
-    if (rc) {
-      (void)wait(i);
-      return rc;
-    }
-  }
-  if (streams) return NET_OK;
-  return wait(ndev);
+  auto enq = [&](int i) -> int {
+    t_enqueueing = true;
+    const int rc = batch_async_s(s, x[i], y[i], B[i], devices[i], streams ? streams[i] : nullptr, ct ? 1 : 0);
+    t_enqueueing = false;
+    return rc;
+  };
+  return multi_driver(ndev, devices, !streams, [&](int d) { return prepare_device(d, s); }, enq, wait);
 }
 }  // namespace
 

@@ -344,6 +344,17 @@ def pack_trials_torch(x, stream=None):
     return y
 
 
+def check_trial_shape(shape, channel_major: bool) -> None:
+    """Raises ValueError unless ``shape`` is a batch of trials in the chosen layout: [B][C][T]
+    (channel-major) or [B][trial_stride] (time-major).  The C ABI sees only pointers and counts, so
+    a batch in the other layout would otherwise run and return wrong logits."""
+    d = _dims()
+    want = (d.C, d.T) if channel_major else (trial_stride(),)
+    if len(shape) != 1 + len(want) or tuple(shape[1:]) != want:
+        kind = f"[B][{d.C}][{d.T}] (channel-major)" if channel_major else f"[B][{want[0]}] (time-major)"
+        raise ValueError(f"trials must be {kind}, got {tuple(shape)}")
+
+
 def model_compute_batch_multi(xs, ys, devices, channel_major: bool = False) -> None:
     """net_model_compute_batch_multi(_ct): xs[i] / ys[i] are device tensors on devices[i]
     ([B_i][trial_stride], or [B_i][C][T] with ``channel_major``, and [B_i][N] int8); one host call
@@ -351,6 +362,11 @@ def model_compute_batch_multi(xs, ys, devices, channel_major: bool = False) -> N
     n = len(devices)
     if not (len(xs) == len(ys) == n):
         raise ValueError("xs, ys and devices must have the same length")
+    d = _dims()
+    for x, y in zip(xs, ys):
+        check_trial_shape(tuple(x.shape), channel_major)
+        if tuple(y.shape) != (x.shape[0], d.N):
+            raise ValueError(f"logits must be [B][{d.N}] per shard, got {tuple(y.shape)}")
     dev = (ctypes.c_int * n)(*devices)
     xp = (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])
     yp = (ctypes.c_void_p * n)(*[y.data_ptr() for y in ys])

@@ -11,8 +11,11 @@ reference's known answer in ``appendix_b.json``.
 The reference ships no vectors of its own (data/*.npz are git-ignored upstream), so these
 fixtures pin the *restatement*; the pin to the reference is the Appendix B known answer.
 """
+import argparse
+import io
 import os
 import sys
+import zipfile
 
 import numpy as np
 
@@ -26,7 +29,20 @@ from mibminet.params import ParamSet, appendix_b_net  # noqa: E402
 OUT = os.path.dirname(os.path.abspath(__file__))
 
 
-def make(name, ps, x):
+def save_npz(path, **arrays):
+    """np.savez_compressed with fixed member timestamps and order, so that regenerating a fixture
+    gives the committed file byte for byte (tests/test_fixtures.py checks it)."""
+    with zipfile.ZipFile(path, "w", compression=zipfile.ZIP_DEFLATED) as z:
+        for name, a in arrays.items():
+            buf = io.BytesIO()
+            np.lib.format.write_array(buf, np.asanyarray(a), allow_pickle=False)
+            info = zipfile.ZipInfo(name + ".npy", date_time=(1980, 1, 1, 0, 0, 0))
+            info.compress_type = zipfile.ZIP_DEFLATED
+            info.external_attr = 0o644 << 16
+            z.writestr(info, buf.getvalue())
+
+
+def make(name, ps, x, out=OUT):
     d = ps.dims
     co = oracle.COracle(ps)
     logits = np.stack([co.model(oracle.to_tc_align(xi, d.C_ALIGN)) for xi in x])
@@ -38,13 +54,13 @@ def make(name, ps, x):
     y3 = co.layer3(y2)
     y3t = co.layer3_flip(y3)
     y4 = co.layer4(y3t)
-    np.savez_compressed(os.path.join(OUT, f"fixture_{name}.npz"),
-                        blob=np.frombuffer(ps.to_blob(), np.uint8), x=x.astype(np.int8),
-                        logits=logits, y1=y1, y2=y2, y3=y3, y3t=y3t, y4=y4)
+    save_npz(os.path.join(out, f"fixture_{name}.npz"),
+             blob=np.frombuffer(ps.to_blob(), np.uint8), x=x.astype(np.int8),
+             logits=logits, y1=y1, y2=y2, y3=y3, y3t=y3t, y4=y4)
     print(name, logits.tolist()[:3])
 
 
-def main():
+def main(out=OUT):
     rng = np.random.default_rng(20250328)
     # config B (22 x 1125), calibrated synthetic parameters, reference test input distribution
     ps = ParamSet.synthetic(seed=11, C=22, T=1125)
@@ -52,23 +68,25 @@ def main():
     x[1] = rng.integers(-128, 128, size=(22, 1125))     # full int8 range
     x[2] = 127
     x[3] = -128
-    make("b22", ps, x)
+    make("b22", ps, x, out=out)
     # config B with the literal SURVEY §8(d) stress ranges (rails, negative truncation)
     ps = ParamSet.synthetic(seed=12, C=22, T=1125, stress=True)
-    make("b22_stress", ps, rng.integers(-128, 128, size=(4, 22, 1125)))
+    make("b22_stress", ps, rng.integers(-128, 128, size=(4, 22, 1125)), out=out)
     # config C (64 x 1000)
     ps = ParamSet.synthetic(seed=13, C=64, T=1000)
-    make("c64", ps, rng.integers(-60, 60, size=(3, 64, 1000)))
+    make("c64", ps, rng.integers(-60, 60, size=(3, 64, 1000)), out=out)
     # config D (22 x 1125, int4 weights)
     ps = ParamSet.synthetic(seed=14, C=22, T=1125, weight_bits=4)
-    make("d22_int4", ps, rng.integers(-128, 128, size=(4, 22, 1125)))
+    make("d22_int4", ps, rng.integers(-128, 128, size=(4, 22, 1125)), out=out)
     # Appendix B parameters (converted from the float QuantLab-style export) with
     # the reference model test's input distribution (test/cl/net/model/testcase.py:53)
     net, cfg, x0 = appendix_b_net(0)
     ps = ParamSet.from_quantlab(net, cfg)
     x = np.concatenate([x0[None], rng.integers(-60, 60, size=(3, 22, 1125))])
-    make("appb", ps, x)
+    make("appb", ps, x, out=out)
 
 
 if __name__ == "__main__":
-    main()
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=OUT, help="output directory (default: tests/golden)")
+    main(ap.parse_args().out)

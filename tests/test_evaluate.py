@@ -64,6 +64,8 @@ def test_argmax_abi_checks():
     buf = (np.zeros(8, np.int8), np.zeros(2, np.int32))
     assert L.net_argmax_batch(buf[0].ctypes.data, buf[1].ctypes.data, 2, 0, 0, None) == lib.NET_ERR_INVALID
     assert L.net_argmax_batch(buf[0].ctypes.data, buf[1].ctypes.data, 2, 65, 0, None) == lib.NET_ERR_INVALID
+    # int trial indices in the kernels: B past INT32_MAX - 4 * 256 is rejected before any launch
+    assert L.net_argmax_batch(buf[0].ctypes.data, buf[1].ctypes.data, 2**31 - 1024, 4, 0, None) == lib.NET_ERR_INVALID
 
 
 @pytest.mark.gpu

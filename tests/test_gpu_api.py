@@ -88,3 +88,64 @@ def test_param_images_bounded_and_reloadable(gpu):
     lib.params_unload()
     lib.params_load(sets[5])
     assert np.array_equal(lib.forward_torch(xd).cpu().numpy(), oracle.COracle(sets[5]).batch(x, nthreads=4))
+
+
+def _upload_stats():
+    L = lib.load()
+    f = L.mibminet_test_upload_stats
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    assert f(ctypes.byref(a), ctypes.byref(b)) == 0
+    return a.value, b.value
+
+
+def test_multi_first_call_uploads_before_enqueue(gpu):
+    """A first multi-device call with a fresh parameter set uploads the image before the first
+    shard is enqueued: no upload (a synchronous copy) happens between enqueues."""
+    import torch
+
+    L = lib.load()
+    ps = ParamSet.synthetic(seed=64)
+    lib.params_load(ps)
+    x = pack_trials(np.random.default_rng(64).integers(-128, 128, size=(64, 22, 1125)))
+    xd = torch.from_numpy(x).cuda()
+    y = torch.zeros((64, 4), dtype=torch.int8, device=gpu)
+    up0, upe0 = _upload_stats()
+    n = 4
+    dev = (ctypes.c_int * n)(*([0] * n))
+    xp = (ctypes.c_void_p * n)(*[xd.data_ptr() + 16 * i * xd.shape[1] for i in range(n)])
+    yp = (ctypes.c_void_p * n)(*[y.data_ptr() + 16 * 4 * i for i in range(n)])
+    bs = (ctypes.c_size_t * n)(*([16] * n))
+    assert L.net_model_compute_batch_multi(n, dev, xp, yp, bs, None) == 0
+    up1, upe1 = _upload_stats()
+    assert up1 == up0 + 1 and upe1 == upe0
+    assert np.array_equal(y.cpu().numpy(), oracle.COracle(ps).batch(x, nthreads=4))
+
+
+def test_param_copy_of_captured_graph_survives_reloads(gpu):
+    """A launch captured into a HIP graph keeps its parameter copy however many other sets are
+    loaded afterwards (the copy is never freed before net_params_unload), while copies that no
+    launch can still read are evicted without a device synchronisation."""
+    import torch
+
+    L = lib.load()
+    L.mibminet_test_device_images.argtypes = [ctypes.c_int]
+    rng = np.random.default_rng(71)
+    x = pack_trials(rng.integers(-128, 128, size=(300, 22, 1125)))
+    xd = torch.from_numpy(x).cuda()
+    sets = [ParamSet.synthetic(seed=710 + i) for i in range(12)]
+    lib.params_load(sets[0])
+    lib.forward_torch(xd)  # uploads set 0 outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            out = lib.forward_torch(xd, stream=s)
+    for ps in sets[1:]:  # 11 more sets: past the 8 copies kept per device
+        lib.params_load(ps)
+        assert np.array_equal(lib.forward_torch(xd).cpu().numpy(), oracle.COracle(ps).batch(x, nthreads=4))
+    assert L.mibminet_test_device_images(0) <= 8
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), oracle.COracle(sets[0]).batch(x, nthreads=4))

@@ -117,3 +117,31 @@ def test_params_load_rejects_nonzero_pads():
     b5[-1] = 0xFF
     assert L.net_params_load(bytes(b5), len(b5)) == lib.NET_ERR_BLOB
     lib.params_unload()
+
+
+def _multi_order(devices, fail_at=-1):
+    L = lib.load()
+    f = L.mibminet_test_multi_order
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    dev = (ctypes.c_int * len(devices))(*devices)
+    buf = ctypes.create_string_buffer(256)
+    rc = f(len(devices), dev, fail_at, buf, 256)
+    return rc, buf.value.decode().split()
+
+
+def test_multi_driver_prepares_every_device_before_enqueueing():
+    """net_model_compute_batch_multi's driver (run with recording stand-ins, no device): every
+    listed device receives the parameter image (P, once per distinct device) before the first
+    shard is enqueued (E), so the first call on a multi-GPU node uploads up front and then starts
+    all devices back to back; then all shards are waited for (W)."""
+    rc, log = _multi_order([0, 1, 2, 3, 4, 5, 6, 7])
+    assert rc == 0
+    assert log == [f"P{d}" for d in range(8)] + [f"E{i}" for i in range(8)] + ["W8"]
+    rc, log = _multi_order([0, 1, 0, 1])
+    assert log == ["P0", "P1", "E0", "E1", "E2", "E3", "W4"]
+
+
+def test_multi_driver_error_waits_for_enqueued_shards_only():
+    rc, log = _multi_order([0, 1, 2, 3], fail_at=2)
+    assert rc == lib.NET_ERR_INVALID
+    assert log == ["P0", "P1", "P2", "P3", "E0", "E1", "E2", "W2"]

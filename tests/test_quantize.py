@@ -98,6 +98,8 @@ def test_pack_abi_checks():
     buf = np.zeros(64, np.int8)
     assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 1, 65, 10, 0, None) == lib.NET_ERR_INVALID
     assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 2**31, 22, 1125, 0, None) == lib.NET_ERR_INVALID
+    # int trial indices in the kernel (b + gridDim.y must not wrap): B <= INT32_MAX - 65,535
+    assert L.net_pack_trials_i8(buf.ctypes.data, buf.ctypes.data, 2**31 - 65535, 22, 1125, 0, None) == lib.NET_ERR_INVALID
     # the output must be 16-byte aligned (the tiles leave as 16-byte stores), and one trial's input
     # must stay below 2 GiB (one buffer view)
     base = (buf.ctypes.data + 15) // 16 * 16

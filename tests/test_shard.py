@@ -82,6 +82,24 @@ def test_multi_abi_checks():
     assert L.net_model_compute_batch_multi(99, None, None, None, None, None) == lib.NET_ERR_INVALID
 
 
+def test_forward_devices_rejects_wrong_layout():
+    """A time-major batch passed as channel-major (or the reverse) is refused before any device
+    work: the C ABI sees only pointers and counts and would return wrong logits."""
+    from mibminet import lib
+    from mibminet.shard import forward_devices
+
+    lib.params_load(ParamSet.synthetic(seed=3))
+    stride = lib.trial_stride()
+    with pytest.raises(ValueError):
+        forward_devices(np.zeros((4, stride), np.int8), [0], channel_major=True)
+    with pytest.raises(ValueError):
+        forward_devices(np.zeros((4, 22, 1125), np.int8), [0], channel_major=False)
+    with pytest.raises(ValueError):
+        lib.check_trial_shape((4, 22, 1000), True)
+    lib.check_trial_shape((4, 22, 1125), True)
+    lib.check_trial_shape((4, stride), False)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("devices,B", [([0], 1000), ([0, 0], 1001), ([0, 0, 0], 515)])
 def test_gpu_forward_devices(gpu, devices, B):
