@@ -117,7 +117,11 @@ struct DevParams {
   // K-slots = the two filters' 96-slot bands side by side (K block diagonal, see forward_wg.hpp)
   v4i l2t_afrag[F2 / 2][3][64];
   SmallParams sp;
-  v4i l1_wfrag_ct[2][64];   // layer-1 B operand for the channel-major staging's window order (Cfg::SG)
+  v4i l1_wfrag_ct[2][64];   // layer-1 B operand for the channel-major staging's K-slot order (stage_block)
+  // layer-2 full-tile and tail bands for the natural-order layer-1 rows (channel-major input with
+  // P == 2, Cfg::L2NAT; for P == 1 every path uses the natural order and l2_afrag / l2t_afrag)
+  v4i l2_afrag_n[F2][3][64];
+  v4i l2t_afrag_n[F2 / 2][3][64];
 };
 
 // LO: lower clip bound, -128 (the C's __CLIP_R(x, 127), clip_balanced=False) or -127

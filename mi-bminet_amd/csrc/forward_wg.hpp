@@ -127,19 +127,29 @@ struct Cfg {
   static constexpr int TB = TAIL ? NB2 - 32 * MT0 : 0;  // tail blocks (of 32 outputs) per filter
   static constexpr int TC = 2 * TB;                     // tail columns (of 16 outputs) per filter
   // layer-1 rows hold positions pos = t + 32 (32 leading zeros = the xcorr pad of 31, aligned).
-  // P == 2: parity-split planes [pos & 1][pos >> 1]: each lane's 4 outputs (one parity) are
-  // contiguous and layer 2's K-window slices are 16-B aligned.
+  // PSPLIT (time-major P == 2): parity-split planes [pos & 1][pos >> 1]: each lane's 4 outputs
+  // (samples of one parity) are contiguous and layer 2's K-window slices are 16-B aligned.
+  // Otherwise (P == 1, and channel-major input, whose layer-1 MFMA rows pair samples j and j + 16,
+  // so that a lane's 4 outputs are consecutive samples) the row is in natural order.
+#ifdef MIB_DIAG_CT_PSPLIT
+  static constexpr bool PSPLIT = P == 2;  // timing proxy (results wrong): the time-major y1 layout
+#else
+  static constexpr bool PSPLIT = P == 2 && !CT_;
+#endif
+  static constexpr int PL = PSPLIT ? 2 : 1;             // y1 layout: planes per row
+  static constexpr bool L2NAT = P == 2 && !PSPLIT;      // layer-2 bands of the natural layout (host: *_n)
   static constexpr int NPOS = cmax(cmax(32 + 16 * P * NB1, 32 * (NB2 - 1) + 96), 1024 * MT + 64);
-  static constexpr int PLANE = align16((NPOS + P - 1) / P);
-  static constexpr int Y1ROW = P * PLANE;
+  static constexpr int PLANE = align16((NPOS + PL - 1) / PL);
+  static constexpr int Y1ROW = PL * PLANE;
   // batched trial stride (bytes): time-major trials are padded to 16 bytes, channel-major ones
   // are the caller's contiguous [B][C][T]
   static constexpr int XTRIAL = FQ ? 4 * C * T : CT ? C * T : align16(T * C);
-  // channel-major staging (layer1, CT): one layer-1 block per wave, time group j at SG j.  P == 2:
-  // window slot 2c + p = channel c of the group's sample p (44 bytes for C = 22); P == 1: slot c.
-  // The last group's window runs 16 bytes past the block (zero weights meet them).
-  static constexpr int SG = P == 2 ? align16(2 * C) : 64;
-  static constexpr int STG = 16 * SG + 16;
+  // channel-major staging (layer1, CT): one layer-1 block per wave, 64 rows of 16 bytes, row =
+  // MFMA K-slot (stage_block)
+#ifndef MIB_CT_DBUF
+#define MIB_CT_DBUF 1
+#endif
+  static constexpr int STG = MIB_CT_DBUF ? 2048 : 1024;  // two areas: block i + 1 is staged under block i
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   // layer 3: tile 1 = the first L3C blocks of both filters side by side (one 16x16x64 MFMA),
   // tile 2 = the L3R outputs past 128, four per column in register 0 only (layer3)
@@ -182,7 +192,7 @@ struct Cfg {
 // byte offset of layer-1 output (filter f, sample t) inside the LDS rows
 template <class K>
 __device__ __forceinline__ int y1_index(int f, int t) {
-  if constexpr (K::P == 2) return f * K::Y1ROW + (t & 1) * K::PLANE + ((t + 32) >> 1);
+  if constexpr (K::PSPLIT) return f * K::Y1ROW + (t & 1) * K::PLANE + ((t + 32) >> 1);
   else return f * K::Y1ROW + 32 + t;
 }
 
@@ -190,7 +200,7 @@ __device__ __forceinline__ int y1_index(int f, int t) {
 // build_lane_tab and re-read every trial with two ds_read_b128: cheaper than recomputing them
 // from the lane id, and registers are too scarce to keep them live across the trial loop.
 struct LaneTab {
-  int l2b;  // full tile, B slice (filter 0, tile 0, K-step 0): (32 / P) c + l2_boff(0, h)
+  int l2b;  // full tile, B slice (filter 0, tile 0, K-step 0): (32 / PL) c + l2_boff(0, h)
   int l2y;  // full tile, y2 store (filter 0, tile 0): 8 + 4 c + 2 h
   int tb[3];  // tail B chunk of K-step s (offset within the wave's filter pair; a zero chunk when
              // the K-step's slots of this lane belong to the other filter)
@@ -247,28 +257,28 @@ __device__ __forceinline__ L45Tab build_l45_tab(int lane) {
 }
 
 // layer-2 B operand: byte offset (within a filter's rows, column block 0) of the 16-byte slice of
-// lane half h, K-step s.  P == 2: half h reads parity plane h, plane bytes 16 s .. 16 s + 15 of the
-// block's window (K-slot 32 s + 16 h + j <-> position 2 (16 s + j) + h); P == 1: natural order.
+// lane half h, K-step s.  PSPLIT: half h reads parity plane h, plane bytes 16 s .. 16 s + 15 of the
+// block's window (K-slot 32 s + 16 h + j <-> position 2 (16 s + j) + h); otherwise natural order.
 // The band fragments built on the host use the same K order.
 template <class K>
 __device__ __forceinline__ int l2_boff(int s, int h) {
-  if constexpr (K::P == 2) return h * K::PLANE + 16 * s;
+  if constexpr (K::PSPLIT) return h * K::PLANE + 16 * s;
   else return 32 * s + 16 * h;
 }
 
 // Layer-2 tail window chunks.  Column (fi, bq) of the tail covers outputs 1024 MT + 16 bq + m
 // (m < 16), which read row positions p0 + q, p0 = 1024 MT + 16 bq, q = m + 1 + tap <= 79.  The
-// window is cut into 16-byte chunks mq = 0..5 of the row: P == 2: plane mq & 1, plane bytes
-// p0 / 2 + 16 (mq >> 1) .. +15 (positions q = 32 (mq >> 1) + 2 jj + (mq & 1)); P == 1: bytes
+// window is cut into 16-byte chunks mq = 0..5 of the row: PSPLIT: plane mq & 1, plane bytes
+// p0 / 2 + 16 (mq >> 1) .. +15 (positions q = 32 (mq >> 1) + 2 jj + (mq & 1)); natural: bytes
 // p0 + 16 mq .. +15 (q = 16 mq + jj; chunk 5 is never needed and reads zeros).  The host builds
 // the band fragments (l2t_afrag) with the same slot -> position map.
 template <class K>
 __device__ __host__ constexpr int tail_q(int mq, int jj) {
-  return K::P == 2 ? 32 * (mq >> 1) + 2 * jj + (mq & 1) : 16 * mq + jj;
+  return K::PSPLIT ? 32 * (mq >> 1) + 2 * jj + (mq & 1) : 16 * mq + jj;
 }
 template <class K>
 __device__ __forceinline__ int tail_chunk_off(int fi, int bq, int mq) {
-  if constexpr (K::P == 2) return fi * K::Y1ROW + (mq & 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (mq >> 1);
+  if constexpr (K::PSPLIT) return fi * K::Y1ROW + (mq & 1) * K::PLANE + 512 * K::MT + 8 * bq + 16 * (mq >> 1);
   else return mq < 5 ? fi * K::Y1ROW + 1024 * K::MT + 16 * bq + 16 * mq : 0;
 }
 
@@ -277,7 +287,7 @@ __device__ __forceinline__ LaneTab build_lane_tab(int lane) {
   LaneTab T;
   {
     const int c = lane & 31, h = lane >> 5;
-    T.l2b = (32 / K::P) * c + l2_boff<K>(0, h);
+    T.l2b = (32 / K::PL) * c + l2_boff<K>(0, h);
     T.l2y = 8 + 4 * c + 2 * h;
   }
   {
@@ -323,6 +333,7 @@ struct Regs {
   float qs, qy;            // float input's quantisation scale and RN(1 / scale) (K::FQ)
   v4i pf[K::PF > 0 ? K::PF : 1];  // layer-1 fragments prefetched one trial ahead
   int xoff;                // lane_xoff(lane)
+  int fq0;                 // float input: slot of the wave's first block in walking order (MIB_FQ_ALT)
 };
 
 // ---- layer-1 input ---------------------------------------------------------------------------
@@ -385,6 +396,12 @@ __device__ __forceinline__ int lane_xoff(int lane, int wave) {
   if constexpr (K::CT) {
     // channel-major: lane (c, h) (P == 2) or c (P == 1) reads 16 samples of channel row c; block
     // slot i adds 16 P i samples.  Lanes past the rows read zeros without a fetch.
+#ifdef MIB_DIAG_CT_TMLOAD
+    // timing proxy (results wrong): every block load reads 16 P C contiguous bytes, as the
+    // time-major path does
+    if (16 * (lane >> 4) >= K::GS) return (int)0x80000000u;
+    return (lane & 15) * K::GS + 16 * (lane >> 4) + 16 * K::GS * l1_start<K>(wave);
+#endif
     const int c = K::P == 2 ? lane >> 1 : lane, h = K::P == 2 ? lane & 1 : 0;
     if (c >= K::C) return (int)0x80000000u;
     return (K::FQ ? 4 : 1) * (c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h);
@@ -409,7 +426,11 @@ __device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
   // cache policy: nt (2) for the time-major stream; none for channel-major, whose 128-byte lines
   // are read by several block loads of a wave (nt: +40 %, tools/ab.py)
   constexpr int AUX = K::CT ? MIB_CT_AUX : 2;
+#ifdef MIB_DIAG_CT_TMLOAD
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * 16 * K::GS, 0, AUX);
+#else
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * (K::CT ? 16 * K::P : 16 * K::GS), 0, AUX);
+#endif
   return (v4i)v;
 }
 
@@ -442,53 +463,50 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// the MFMA A fragment of the block staged at stg (time group j = lane & 15, bytes 16 (lane >> 4))
-template <class K>
-__device__ __forceinline__ v4i staged_a(const int8_t* stg, int lane) {
-  return *(const v4i*)(stg + K::SG * (lane & 15) + 16 * (lane >> 4));
+// Channel-major staging: the A operand of a layer-1 block through LDS, transposed by the hardware.
+// A K-slot's row is 16 consecutive samples of one channel, which is what a lane loads: P == 2:
+// lane L = (channel L >> 1, half h = L & 1) holds samples 32 blk + 16 h .. +15, and K-slot L is
+// channel L >> 1 at sample 16 h + j of MFMA row j (rows pair samples j and j + 16); P == 1: lane c
+// = channel c, samples 16 blk .. +15, K-slot c.  Each lane stores its row with one ds_write_b128,
+// and two ds_read_b64_tr_b8 return the fragment: per 16-lane group g, an 8-row x 16-column byte
+// block read column-wise, so lane (j, g) receives byte j of K-slots 16 g .. 16 g + 7, then
+// 16 g + 8 .. 16 g + 15 (tools/tr8_probe.hip checks the form).  Physical row of K-slot
+// k = 16 g + 8 r + q is stg_pos(k) = 16 g + 8 (r ^ (g & 1)) + q: the two groups of a 32-lane half
+// then read different bank halves (conflict-free); stg_pos is its own inverse.
+__device__ __forceinline__ int stg_pos(int k) { return k ^ ((k >> 1) & 8); }
+
+#ifndef MIB_TR8_QSEL
+#define MIB_TR8_QSEL 0
+#endif
+// byte offsets of lane (i, g)'s two transposed reads: lane i of a group supplies the address of
+// row q, bytes 8 p .. 8 p + 7 of its 8-row block
+__device__ __forceinline__ int stg_read_off(int lane, int r) {
+  const int i = lane & 15, g = lane >> 4;
+  const int q = MIB_TR8_QSEL ? (i & 7) : (i >> 1), p = MIB_TR8_QSEL ? (i >> 3) : (i & 1);
+  return 16 * stg_pos(16 * g + 8 * r + q) + 8 * p;
 }
 
-// One layer-1 block: the lane's 16 samples of channel c go to the wave's staging area in the
-// window layout of Cfg::SG and come back as the block's MFMA A fragment (one ds_read_b128).
-//  P == 2 (window slot 2c + p = channel c of the group's sample p): lanes (c, h) and (c ^ 1, h)
-//    trade dwords by DPP (partner lane L ^ 2), and one v_perm forms a time group's 4 bytes of the
-//    channel pair; 4 dword stores per lane (-4.9 % against 8 two-byte stores straight from the
-//    loaded dwords; tools/ab.py --ct).
-//  P == 1 (slot c): a 4 x 4 byte transpose inside each lane quad (channels c0 .. c0 + 3, dword k
-//    = samples 4k .. 4k + 3) in two DPP + v_perm stages (partner L ^ 1, then L ^ 2); lane q then
-//    holds sample 4k + q of the quad's four channels and stores it as one dword (-1 % / -2 % on
-//    64x1000 / 64x480 against 2-byte pair stores, which were -5.6 % / -15 % against byte stores).
 template <class K>
 __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
-  wave_sync_lds();  // the previous block's A reads precede these stores
-  if constexpr (K::P == 2) {
-    static_assert(K::C % 2 == 0, "channel pairs");
-    const int c = lane >> 1;
-    const unsigned sel = (c & 1) ? 0x03020706u : 0x05040100u;
-    int8_t* p = stg + 8 * K::SG * (lane & 1) + 2 * (c & ~1) + K::SG * (c & 1);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {  // dword k: samples 4k .. 4k + 3 = time groups 2k, 2k + 1
-      const unsigned d = (unsigned)raw[k];
-      const unsigned w = __builtin_amdgcn_perm((unsigned)__builtin_amdgcn_mov_dpp((int)d, 0x4E, 0xF, 0xF, false), d, sel);
-      if (lane < 2 * K::C) *(unsigned*)(p + 2 * K::SG * k) = w;  // the even channel's lane: group 2k
-    }
-  } else {
-    static_assert(K::C % 4 == 0, "channel quads");
-    const unsigned sel1 = (lane & 1) ? 0x03070105u : 0x06020400u;
-    const unsigned sel2 = (lane & 2) ? 0x03020706u : 0x05040100u;
-    int8_t* p = stg + (lane & ~3) + K::SG * (lane & 3);
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const unsigned d = (unsigned)raw[k];
-      const unsigned a = __builtin_amdgcn_perm((unsigned)__builtin_amdgcn_mov_dpp((int)d, 0xB1, 0xF, 0xF, false), d, sel1);
-      const unsigned w = __builtin_amdgcn_perm((unsigned)__builtin_amdgcn_mov_dpp((int)a, 0x4E, 0xF, 0xF, false), a, sel2);
-      if (lane < K::C) *(unsigned*)(p + 4 * K::SG * k) = w;
-    }
-  }
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  wave_sync_lds();  // the previous block's reads precede this store
+  *(v4i*)(stg + 16 * stg_pos(lane)) = raw;
   wave_sync_lds();
-  return staged_a<K>(stg, lane);
+  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 0)));
+  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 1)));
+  return (v4i){lo[0], lo[1], hi[0], hi[1]};
 }
 
+#ifndef MIB_FQ_ALT
+#define MIB_FQ_ALT 0
+#endif
+// float input: where the next trial's first block is requested: 1 at the end of layer 1, 2 after
+// layer 2, 3 after layer 3 (a later request leaves less time for its shared cache lines to leave
+// L2 before the rest of the trial's blocks read them)
+#ifndef MIB_FQ_PF_AT
+#define MIB_FQ_PF_AT 1
+#endif
 // float input (K::FQ): 16-byte piece m of the lane's 64 bytes of block slot i
 template <class K>
 __device__ __forceinline__ v4i load_f(Rsrc r, int xoff, int i, int m) {
@@ -503,7 +521,7 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R) {
   asm volatile("" : "+v"(xo));
   if constexpr (K::FQ) {  // the first block's four pieces
 #pragma unroll
-    for (int m = 0; m < 4; m++) R.pf[m] = load_f<K>(r, xo, 0, m);
+    for (int m = 0; m < 4; m++) R.pf[m] = load_f<K>(r, xo, R.fq0, m);
     return;
   }
 #pragma unroll
@@ -526,7 +544,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   for (int fi = 0; fi < FPW; fi++) {
     const int f = wave * FPW + fi;
 #pragma unroll
-    for (int s = 0; s < 3; s++) R.af[fi][s] = prm->l2_afrag[f][s][lane];
+    for (int s = 0; s < 3; s++) R.af[fi][s] = K::L2NAT ? prm->l2_afrag_n[f][s][lane] : prm->l2_afrag[f][s][lane];
     if constexpr (K::RB) {
       R.thr2[fi] = prm->l2_thrb[f];
       R.off2[fi] = prm->l2_offm[f];
@@ -537,6 +555,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
       R.r2[fi] = prm->sp.l2n_r[f];
     }
   }
+  R.fq0 = (MIB_FQ_ALT && (wave & 1)) ? l1_count<K>(wave) - 1 : 0;
   R.a31 = prm->l3_a1[wave][lane];
   R.a32 = prm->l3_a2[wave][lane];
   R.r3 = prm->sp.l3_r;
@@ -548,7 +567,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   if (tid < 64) ((LaneTab*)(smem + K::OFF_LT))[tid] = build_lane_tab<K>(tid);
   if (tid < 64) ((L45Tab*)(smem + K::OFF_L45))[tid] = build_l45_tab<K>(tid);
   if constexpr (K::TB > 0) {
-    const v4i* t = &prm->l2t_afrag[0][0][0];
+    const v4i* t = K::L2NAT ? &prm->l2t_afrag_n[0][0][0] : &prm->l2t_afrag[0][0][0];
     v4i* d = (v4i*)(smem + K::OFF_L2T);
     for (int i = tid; i < NWAVES * 3 * 64; i += NTHREADS) d[i] = t[i];
   }
@@ -584,11 +603,16 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
   for (int t = 0; t < K::P; t++) {
     const L1Tile& T = R.tile(t);
     const v4i acc = accs[t];
+    // lane column j = (filter 8t + j/2, parity or half j&1) when P == 2, filter j when P == 1.
+    // Row 4g + r: time-major, time group 16 blk + 4g + r (its sample p when P == 2: stride 2);
+    // channel-major P == 2: sample 32 blk + 16 p + 4g + r (consecutive).
+    const int p = (K::P == 2) ? (j & 1) : 0;
+    const int f = (K::P == 2) ? 8 * t + (j >> 1) : j;
+    const int t0 = K::PSPLIT ? 2 * (16 * blk + 4 * g) + p : K::P == 2 ? 32 * blk + 16 * p + 4 * g : 16 * blk + 4 * g;
+    constexpr int SS = K::PL;  // sample stride of the lane's 4 outputs
 #ifdef MIB_DIAG_NOL1RQ
     {
-      const int p = (K::P == 2) ? (j & 1) : 0;
-      const int f = (K::P == 2) ? 8 * t + (j >> 1) : j;
-      *(unsigned*)(smem_y1 + y1_index<K>(f, K::P * (16 * blk + 4 * g) + p)) = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
+      *(unsigned*)(smem_y1 + y1_index<K>(f, t0)) = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
       continue;
     }
 #endif
@@ -596,15 +620,10 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
     const f2 q01 = fma2(acc[0], acc[1], T.rr, T.cc);
     const f2 q23 = fma2(acc[2], acc[3], T.rr, T.cc);
     int y[4] = {(int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]};  // trunc toward zero
-    // lane column j = (filter 8t + j/2, parity j&1) when P == 2, filter j when P == 1;
-    // row 4g + r = time group 16 blk + 4g + r
-    const int p = (K::P == 2) ? (j & 1) : 0;
-    const int f = (K::P == 2) ? 8 * t + (j >> 1) : j;
     if constexpr (MAYBE_LAST) {
 #pragma unroll
-      for (int r = 0; r < 4; r++) y[r] = (K::P * (16 * blk + 4 * g + r) + p < K::T) ? y[r] : 0;
+      for (int r = 0; r < 4; r++) y[r] = (t0 + SS * r < K::T) ? y[r] : 0;
     }
-    const int t0 = K::P * (16 * blk + 4 * g) + p;  // first of the lane's 4 samples (stride P)
     *(unsigned*)(smem_y1 + y1_index<K>(f, t0)) = sat8x4<K::LO>(y[0], y[1], y[2], y[3]);
   }
 }
@@ -689,14 +708,17 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     const int n = l1_count<K>(wave);
     int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;
     v4i cur[4] = {R.pf[0], R.pf[1], R.pf[2], R.pf[3]};
+    // MIB_FQ_ALT: odd waves walk their blocks backwards (slot n - 1 first), so that both sides of
+    // every wave border are read in the same phase of the trial (float input)
+    const bool back = MIB_FQ_ALT && (wave & 1);
 #pragma unroll
     for (int i = 0; i < K::NBW; i++) {
       if (i < n) {  // wave-uniform
-        const int blk = l1_blk<K>(wave, i);
+        const int blk = l1_blk<K>(wave, back ? n - 1 - i : i);
         v4i nxt[4] = {cur[0], cur[1], cur[2], cur[3]};
         if (i + 1 < n)
 #pragma unroll
-          for (int m = 0; m < 4; m++) nxt[m] = load_f<K>(rcur, R.xoff, i + 1, m);
+          for (int m = 0; m < 4; m++) nxt[m] = load_f<K>(rcur, R.xoff, back ? n - 2 - i : i + 1, m);
         v4i raw;
 #pragma unroll
         for (int m = 0; m < 4; m++) raw[m] = (int)quantize4(cur[m], R.qs, R.qy);
@@ -710,7 +732,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         for (int m = 0; m < 4; m++) cur[m] = nxt[m];
       }
     }
-    prefetch_l1<K>(rnext, R);
+    if (MIB_FQ_PF_AT == 1) prefetch_l1<K>(rnext, R);  // else from the trial loop (k_forward)
     return;
   }
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
@@ -719,6 +741,40 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
   for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
   int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;  // channel-major staging
+  if constexpr (K::CT && MIB_CT_DBUF) {
+    // block i + 1 is staged (store + transposed reads) before block i's MFMAs and requant, so the
+    // LDS round trip of the staging overlaps the previous block's work (two staging areas)
+    auto raw = [&](int i) -> v4i {
+      v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
+      if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
+      return a;
+    };
+#ifdef MIB_DIAG_CT_NOSTAGE
+    v4i an = raw(0);  // timing proxy (results wrong): the A fragment straight from the loads
+#else
+    v4i an = stage_block<K>(raw(0), stg, lane);
+#endif
+#pragma unroll
+    for (int i = 0; i < K::NBW; i++) {
+      if (i < n) {  // wave-uniform
+        const int blk = l1_blk<K>(wave, i);
+        const v4i a = an;
+        if (i + 1 < n)
+#ifdef MIB_DIAG_CT_NOSTAGE
+          an = raw(i + 1);
+#else
+          an = stage_block<K>(raw(i + 1), stg + 1024 * ((i + 1) & 1), lane);
+#endif
+        if (blk == K::NB1 - 1) {
+          l1_block<K, true>(a, blk, smem_y1, R, lane);
+        } else {
+          l1_block<K, false>(a, blk, smem_y1, R, lane);
+        }
+      }
+    }
+    prefetch_l1<K>(rnext, R);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < K::NBW; i++) {
     if (i < n) {  // wave-uniform
@@ -842,10 +898,28 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 #pragma unroll
     for (int fi = 0; fi < FPW; fi++) {
       const int f = wave * FPW + fi;
-      const int8_t* pb = smem_y1 + f * K::Y1ROW + (32 / K::P) * 32 * mt + T.l2b - l2_boff<K>(0, 0);
+      const int8_t* pb = smem_y1 + f * K::Y1ROW + (32 / K::PL) * 32 * mt + T.l2b - l2_boff<K>(0, 0);
       v16i acc;
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = K::RB ? pbias(fi) : R.thr2[fi];  // plain branch: C-init
+#ifdef MIB_DIAG_L2_16
+      {  // timing/energy proxy (results wrong): the full tile's 1024 outputs in the 16x16x64 shape
+         // at the same outputs per wave.  16 shifts need a 79-position window, so K = 128: 4 column
+         // tiles of 16 blocks x 2 K-steps = 8 MFMAs and 8 B reads (against 3 + 3 for 32x32x32).
+        v4i q[4];
+#pragma unroll
+        for (int ct = 0; ct < 4; ct++) {
+          v4i c4 = {pbias(fi), pbias(fi), pbias(fi), pbias(fi)};
+#pragma unroll
+          for (int ks = 0; ks < 2; ks++)
+            c4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(R.af[fi][ks], *(const v4i*)(pb + 256 * ct + 64 * ks), c4, 0, 0, 0);
+          q[ct] = c4;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc[i] = q[i >> 2][i & 3];
+      }
+      if constexpr (false)
+#endif
 #pragma unroll
       for (int s = 0; s < 3; s++)
 #ifdef MIB_DIAG_NOL2MFMA
@@ -1146,6 +1220,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
 #ifndef MIB_DIAG_NOL2
     layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, T, wave, ln);
 #endif
+    if constexpr (K::FQ && MIB_FQ_PF_AT == 2) prefetch_l1<K>(rn, R);
     // layer 3 of filter f reads only y2 row f, which this wave wrote
 #ifdef MIB_DIAG_L23BAR
     __syncthreads();
@@ -1164,6 +1239,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
 #ifndef MIB_DIAG_NOL3
     layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, T, wave);
 #endif
+    if constexpr (K::FQ && MIB_FQ_PF_AT == 3) prefetch_l1<K>(rn, R);
 #if MIB_PRIO_L3 && !MIB_PRIO_L3_NORESET
     __builtin_amdgcn_s_setprio(0);
 #endif

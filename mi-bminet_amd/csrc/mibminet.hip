@@ -333,8 +333,9 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         bytes[jj] = (int8_t)((c >= 0 && c < C) ? w1(f, c) : 0);
       }
       std::memcpy(&dp.l1_wfrag[t][lane], bytes, 16);
-      // channel-major staging (forward_wg.hpp, stage_block): P == 2 window slot 2c + p holds
-      // channel c of sample p; P == 1 is the same slot order as above
+      // channel-major staging (forward_wg.hpp, stage_block): P == 2 K-slot 2c + p holds channel
+      // c at sample 16 p + j of MFMA row j (column parity p selects it); P == 1 is the same slot
+      // order as above
       for (int jj = 0; jj < 16; jj++) {
         const int k = 16 * g + jj;
         const int c = P == 2 ? k >> 1 : k, pk = P == 2 ? k & 1 : 0;
@@ -350,23 +351,51 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     }
   }
   // layer 2: A operand = banded weights; row i <-> shift n(i) so that lane (c, h) register r
-  // holds output shift 16h + r (two complete pool-8 windows per lane).
-  for (int f = 0; f < F2; f++) {
-    for (int s = 0; s < 3; s++)
-      for (int lane = 0; lane < 64; lane++) {
-        const int i = lane & 31, hh = lane >> 5;
-        const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
-        int8_t bytes[16];
-        for (int jj = 0; jj < 16; jj++) {
-          const int kq = 32 * s + 16 * hh + jj;  // K-slot
-          // position in the 96-byte row window.  P == 2: lane half hh reads
-          // parity plane hh, bytes 16s .. 16s+15 of the block's window; P == 1: natural order.
-          const int kp = P == 2 ? 2 * (16 * s + jj) + hh : kq;
-          const int idx = kp - n - 1;            // tap (torch order)
-          bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
+  // holds output shift 16h + r (two complete pool-8 windows per lane).  PL: layer-1 row layout,
+  // 2 = parity-split planes (time-major input, C <= 32), 1 = natural order; both are built (the
+  // channel-major kernel of a C <= 32 network uses the natural one, l2_afrag_n).
+  auto l2_bands = [&](int PL, v4i (*afrag)[3][64]) {
+    for (int f = 0; f < F2; f++)
+      for (int s = 0; s < 3; s++)
+        for (int lane = 0; lane < 64; lane++) {
+          const int i = lane & 31, hh = lane >> 5;
+          const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
+          int8_t bytes[16];
+          for (int jj = 0; jj < 16; jj++) {
+            const int kq = 32 * s + 16 * hh + jj;  // K-slot
+            // position in the 96-byte row window.  PL == 2: lane half hh reads
+            // parity plane hh, bytes 16s .. 16s+15 of the block's window; PL == 1: natural order.
+            const int kp = PL == 2 ? 2 * (16 * s + jj) + hh : kq;
+            const int idx = kp - n - 1;            // tap (torch order)
+            bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
+          }
+          std::memcpy(&afrag[f][s][lane], bytes, 16);
         }
-        std::memcpy(&dp.l2_afrag[f][s][lane], bytes, 16);
-      }
+  };
+  // layer-2 tail bands (forward_wg.hpp, layer2_tail_mfma): filter pair w = filters 2w, 2w+1;
+  // lane (m, g) of K-step s holds K-slots 64 s + 16 g + jj = chunk kap = 4 s + g, byte jj, which
+  // is chunk mq = kap - 6 kf of filter kf = kap / 6; its window position q (tail_q) meets tap
+  // q - m - 1 of the output shift m.
+  auto l2_tail_bands = [&](int PL, v4i (*tfrag)[3][64]) {
+    for (int w = 0; w < F2 / 2; w++)
+      for (int s = 0; s < 3; s++)
+        for (int lane = 0; lane < 64; lane++) {
+          const int m = lane & 15, g = lane >> 4, kap = 4 * s + g, kf = kap / 6, mq = kap - 6 * kf;
+          const int f = 2 * w + kf;
+          int8_t bytes[16];
+          for (int jj = 0; jj < 16; jj++) {
+            const int q = PL == 2 ? 32 * (mq >> 1) + 2 * jj + (mq & 1) : 16 * mq + jj;
+            const int idx = q - m - 1;
+            bytes[jj] = (int8_t)((idx >= 0 && idx < 64 && (PL == 2 || mq < 5)) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
+          }
+          std::memcpy(&tfrag[w][s][lane], bytes, 16);
+        }
+  };
+  l2_bands(P, dp.l2_afrag);
+  l2_bands(1, dp.l2_afrag_n);
+  l2_tail_bands(P, dp.l2t_afrag);
+  l2_tail_bands(1, dp.l2t_afrag_n);
+  for (int f = 0; f < F2; f++) {
     // pooling in the biased relu form (forward_common.hpp, pool8): thr = -(off >> 3) (layer2.c)
     const int32_t thr2 = -(hp.l2_offset[f] >> 3);
     dp.l2_thrb[f] = pbias(f & 1) + thr2;  // the wave's filter slot f & 1 (forward_wg.hpp, layer2)
@@ -379,23 +408,6 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     dp.sp.l2_tpar[f] = (v4i){PBIAS_TAIL + thr2, dp.l2_offm[f], rbits, 0};
 
   }
-  // layer-2 tail bands (forward_wg.hpp, layer2_tail_mfma): filter pair w = filters 2w, 2w+1;
-  // lane (m, g) of K-step s holds K-slots 64 s + 16 g + jj = chunk kap = 4 s + g, byte jj, which
-  // is chunk mq = kap - 6 kf of filter kf = kap / 6; its window position q (tail_q) meets tap
-  // q - m - 1 of the output shift m.
-  for (int w = 0; w < F2 / 2; w++)
-    for (int s = 0; s < 3; s++)
-      for (int lane = 0; lane < 64; lane++) {
-        const int m = lane & 15, g = lane >> 4, kap = 4 * s + g, kf = kap / 6, mq = kap - 6 * kf;
-        const int f = 2 * w + kf;
-        int8_t bytes[16];
-        for (int jj = 0; jj < 16; jj++) {
-          const int q = P == 2 ? 32 * (mq >> 1) + 2 * jj + (mq & 1) : 16 * mq + jj;
-          const int idx = q - m - 1;
-          bytes[jj] = (int8_t)((idx >= 0 && idx < 64 && (P == 2 || mq < 5)) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
-        }
-        std::memcpy(&dp.l2t_afrag[w][s][lane], bytes, 16);
-      }
   SmallParams& sp = dp.sp;
   // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed.  A
   // operand of MFMA i32_16x16x64_i8 (forward_wg.hpp, layer3): row r, K-slot k of filter f's half

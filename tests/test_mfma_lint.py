@@ -98,3 +98,28 @@ def test_no_inline_asm_hazard_next_to_mfma(tmp_path):
                        check=True, capture_output=True, text=True)
     hazards = [l for l in r.stdout.splitlines() if "asm write into" in l]
     assert not hazards, "\n".join(hazards)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+def test_layer1_cinit_not_written_near_loads(tmp_path):
+    """The round-1 layer-1 fault's remaining candidate: an MFMA C-init written by a
+    VALU instruction a few wait states before the MFMA while loads are outstanding.  In every
+    k_forward instantiation (time-major, channel-major, float input; all build variants) the
+    layer-1 C-inits are built once before the trial loop (where a full drain precedes the first
+    layer 1), so no layer-1 MFMA may show the pattern (tools/cinit_scan.py)."""
+    import cinit_scan
+
+    asm = tmp_path / "mibminet.s"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-function",
+                    "-mllvm", "-disable-promote-alloca-to-lds", "--cuda-device-only", "-S", "-o", str(asm),
+                    os.path.join(ROOT, "mi-bminet_amd", "csrc", "mibminet.hip")],
+                   check=True, capture_output=True)
+    with open(os.devnull, "w") as null:
+        old, sys.stdout = sys.stdout, null
+        try:
+            hits = cinit_scan.scan(cinit_scan.parse(str(asm)), [])
+        finally:
+            sys.stdout = old
+    funcs = [n for n in cinit_scan.parse(str(asm)) if "k_forward" in n]
+    assert len(funcs) == 36
+    assert not [h for h in hits if h[1] == 1], [h for h in hits if h[1] == 1]

@@ -4,7 +4,7 @@ block inside each segment).  Usage: make -C mi-bminet_amd asm && python tools/is
 import re
 import sys
 
-cfg = sys.argv[1] if len(sys.argv) > 1 else "22ELi1125ELb1ELb0"
+cfg = sys.argv[1] if len(sys.argv) > 1 else "22ELi1125ELb1ELb0ELb0ELb0"
 s = open("mi-bminet_amd/build/mibminet.s").read()
 names = re.findall(r"^(_ZN3mib2wg9k_forward\S*):", s, re.M)
 name = [n for n in names if cfg in n][0]
