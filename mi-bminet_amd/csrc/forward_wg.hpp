@@ -498,14 +498,20 @@ __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   return (v4i){lo[0], lo[1], hi[0], hi[1]};
 }
 
+// Float input, HBM traffic (float input; pmc_traffic.json b22_f32).  Float rows are
+// not 128-byte aligned, so a cache line at a border between two blocks holds bytes of both.  With
+// every wave walking forward, the next wave's first block was requested a trial ahead while this
+// wave's last block arrived at the end of layer 1, and each such line came from HBM twice (1.23x).
+// MIB_FQ_ALT: odd waves walk their blocks backwards, so both sides of every wave border are read
+// in the same phase of the trial.  MIB_FQ_PF_AT: where the next trial's first block is requested:
+// 1 at the end of layer 1, 2 after layer 2, 3 after layer 3; a later request leaves less time for
+// the line it shares with the block loaded next to leave L2.  Same box: 1.231x -> 1.089x (ALT) ->
+// 1.021x (ALT + PF_AT 2), -6.9 % time (tools/ab.py --f32, profiles/r04_ab.txt).
 #ifndef MIB_FQ_ALT
-#define MIB_FQ_ALT 0
+#define MIB_FQ_ALT 1
 #endif
-// float input: where the next trial's first block is requested: 1 at the end of layer 1, 2 after
-// layer 2, 3 after layer 3 (a later request leaves less time for its shared cache lines to leave
-// L2 before the rest of the trial's blocks read them)
 #ifndef MIB_FQ_PF_AT
-#define MIB_FQ_PF_AT 1
+#define MIB_FQ_PF_AT 2
 #endif
 // float input (K::FQ): 16-byte piece m of the lane's 64 bytes of block slot i
 template <class K>
