@@ -402,6 +402,12 @@ __device__ __forceinline__ int lane_xoff(int lane, int wave) {
     if (16 * (lane >> 4) >= K::GS) return (int)0x80000000u;
     return (lane & 15) * K::GS + 16 * (lane >> 4) + 16 * K::GS * l1_start<K>(wave);
 #endif
+#ifdef MIB_DIAG_CT_PAIR64
+    // timing proxy (results wrong): the load pattern of block pairs, 11 rows x 64 bytes per load
+    // (lane (c, k): channel c (+ 11 for odd slots), bytes 16 k of the pair)
+    if (lane >= 44) return (int)0x80000000u;
+    return (lane >> 2) * K::T + 16 * (lane & 3) + 32 * l1_start<K>(wave);
+#endif
     const int c = K::P == 2 ? lane >> 1 : lane, h = K::P == 2 ? lane & 1 : 0;
     if (c >= K::C) return (int)0x80000000u;
     return (K::FQ ? 4 : 1) * (c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h);
@@ -428,6 +434,8 @@ __device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
   constexpr int AUX = K::CT ? MIB_CT_AUX : 2;
 #ifdef MIB_DIAG_CT_TMLOAD
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * 16 * K::GS, 0, AUX);
+#elif defined(MIB_DIAG_CT_PAIR64)
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff, (i & 1) * 11 * K::T + 64 * (i >> 1), AUX);
 #else
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * (K::CT ? 16 * K::P : 16 * K::GS), 0, AUX);
 #endif
@@ -491,7 +499,13 @@ __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   typedef int v2i __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) v2i lds_v2i;
   wave_sync_lds();  // the previous block's reads precede this store
+#ifdef MIB_DIAG_CT_NOWRITE
+  // timing proxy (results wrong): the transposed reads without the store (what an LDS-DMA fill,
+  // which needs no VGPR -> LDS transfer, could at most save); the loaded data is kept live
+  asm volatile("" ::"v"(raw));
+#else
   *(v4i*)(stg + 16 * stg_pos(lane)) = raw;
+#endif
   wave_sync_lds();
   const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 0)));
   const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 1)));

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--B", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--settle", type=float, default=1.0, help="seconds of untimed launches before round 0")
     ap.add_argument("--variant", default="canonical", choices=("canonical", "plain_bn", "clip_balanced"))
     ap.add_argument("--ct", action="store_true", help="channel-major input (net_model_compute_batch_ct)")
     ap.add_argument("--f32", action="store_true", help="float32 channel-major input (net_model_compute_batch_f32)")
@@ -67,6 +68,15 @@ def main():
     for p, o in zip(a.libs, outs):
         same = bool(torch.equal(o, outs[0]))
         print(f"{os.path.basename(p):28s} output {'==' if same else '!='} first library's", flush=True)
+    # settle the clock (power cap) before the first timed round: without it the first library of
+    # the first rounds can read a few per cent slow (identical libraries differed by up to 3.7 %)
+    import time
+    t0 = time.time()
+    while time.time() - t0 < a.settle:
+        for L in libs:
+            for _ in range(10):
+                L.net_model_compute_batch_async(x.data_ptr(), y.data_ptr(), a.B, 0, st.cuda_stream)
+        torch.cuda.synchronize()
     times = {p: [] for p in a.libs}
     for r in range(a.rounds):
         for p, L in zip(a.libs, libs):
