@@ -43,7 +43,7 @@ def main():
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(one(f"{src}/trace/**/*kernel_stats.csv"), f"{prof}/{tag}_kernel_stats.csv")
-    for cfg in ("b22", "c64", "d22", "p64"):
+    for cfg in ("b22", "c64", "d22", "p64", "b22_ct", "c64_ct", "b22_f32"):
         p = f"{src}/bench_{cfg}.json"
         if os.path.exists(p):
             lines = [l for l in open(p) if l.startswith("{")]
@@ -53,10 +53,13 @@ def main():
     rcols = ("TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")
     # skip the first (warm-up) dispatch
     med = lambda v: sorted(v[1:] or v)[len(v[1:] or v) // 2]  # noqa: E731
-    alg = {"b22": 22 * 1125 + 4, "c64": 64 * 1000 + 4, "d22": 22 * 1125 + 4}
-    kern = {"b22": (22, 1125), "c64": (64, 1000), "d22": (22, 1125)}
+    alg = {"b22": 22 * 1125 + 4, "c64": 64 * 1000 + 4, "d22": 22 * 1125 + 4,
+           "b22_ct": 22 * 1125 + 4, "c64_ct": 64 * 1000 + 4, "b22_f32": 4 * 22 * 1125 + 4}
+    kern = {"b22": "22,1125,RB=1,CB=0", "c64": "64,1000,RB=1,CB=0", "d22": "22,1125,RB=1,CB=0",
+            "b22_ct": "22,1125,RB=1,CB=0,CT=1", "c64_ct": "64,1000,RB=1,CB=0,CT=1",
+            "b22_f32": "22,1125,RB=1,CB=0,CT=1,FQ=1"}
     configs = {}
-    for cfg in ("b22", "c64", "d22"):
+    for cfg in ("b22", "c64", "d22", "b22_ct", "c64_ct", "b22_f32"):
         wf = glob.glob(f"{src}/pmc_write_{cfg}/**/*counter_collection.csv", recursive=True)
         rq = glob.glob(f"{src}/pmc_rdreq_{cfg}/**/*counter_collection.csv", recursive=True)
         if not (wf and rq):
@@ -74,7 +77,7 @@ def main():
         # sizes, if any, are reported as the remainder and not counted); writes WRITE_SIZE (kB)
         read_bytes = 32 * n[rcols[1]] + 64 * n[rcols[2]] + 128 * n[rcols[3]]
         write_bytes = med(write) * 1024
-        tc = {"batch": 65536, "kernel": "k_forward<Cfg<%d,%d,RB=1,CB=0>>" % kern[cfg],
+        tc = {"batch": 65536, "kernel": "k_forward<Cfg<%s>>" % kern[cfg],
               "rdreq": n, "rdreq_other": n[rcols[0]] - n[rcols[1]] - n[rcols[2]] - n[rcols[3]],
               "read_bytes": read_bytes, "write_bytes": write_bytes,
               "alg_bytes_per_launch": alg[cfg] * 65536,

@@ -17,17 +17,25 @@ for cfg in c64 d22; do
   cat "$OUT/bench_$cfg.json"
 done
 timeout -k 10 200 $B --steps 50 --warmup 5 --config p64 --no-cpu-baseline > "$OUT/bench_p64.json" 2>> "$OUT/bench.err" || exit $?
+# the other input layouts: channel-major int8 (B, C) and float32 (B)
+for cl in b22:ct c64:ct b22:f32; do
+  cfg=${cl%%:*}; lay=${cl#*:}
+  timeout -k 10 200 $B --steps 50 --warmup 5 --config $cfg --layout $lay --no-cpu-baseline > "$OUT/bench_${cfg}_${lay}.json" 2>> "$OUT/bench.err" || exit $?
+  cat "$OUT/bench_${cfg}_${lay}.json"
+done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- \
   python3 "$ROOT/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > "$OUT/trace.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
   python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/pmc_fetch.log" 2>&1 || exit $?
-for cfg in b22 c64 d22; do
-  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$cfg" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --config $cfg > "$OUT/pmc_write_$cfg.log" 2>&1 || exit $?
+for cl in b22 c64 d22 b22:ct c64:ct b22:f32; do
+  cfg=${cl%%:*}; lay=tc; [ "$cl" != "$cfg" ] && lay=${cl#*:}
+  key=$cfg; [ $lay != tc ] && key=${cfg}_$lay
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_$key" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --config $cfg --layout $lay > "$OUT/pmc_write_$key.log" 2>&1 || exit $?
   # read requests by size (32/64/128 B): the byte count without FETCH_SIZE's fixed-size assumption
   timeout -k 10 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum \
-    -d "$OUT/pmc_rdreq_$cfg" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --config $cfg > "$OUT/pmc_rdreq_$cfg.log" 2>&1 || exit $?
+    -d "$OUT/pmc_rdreq_$key" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --config $cfg --layout $lay > "$OUT/pmc_rdreq_$key.log" 2>&1 || exit $?
 done
 find "$OUT" -name "*.csv" | sort
