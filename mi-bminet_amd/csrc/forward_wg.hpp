@@ -117,6 +117,15 @@ struct Cfg {
   // of which prefetched a trial ahead (the plain-BN builds hold more per-filter state)
   // (float input: the first block's four 16-byte pieces; the others load one block ahead)
   static constexpr int PF = FQ_ ? 4 : cmin(NBW, RB ? PF_MAX : CT_ ? MIB_PF_MAX_PLAIN_CT : MIB_PF_MAX_PLAIN);
+#ifndef MIB_CT_PAIRS
+#define MIB_CT_PAIRS 0
+#endif
+  // channel-major int8, P == 2, every block prefetched: blocks 2j, 2j + 1 are loaded as a pair, two
+  // loads of C / 2 rows x 64 bytes (layer1, stage_pair); an odd last block alone.  Off: same box
+  // +3.3 % against the double-buffered single blocks (a timing proxy of the load pattern alone had
+  // promised -3.2 %; the pair gives up the staging overlap and its stores scatter)
+  static constexpr bool PAIRS = MIB_CT_PAIRS && CT_ && !FQ_ && P == 2 && PF == NBW && NBW >= 2 && C % 2 == 0;
+  static constexpr int NPAIR = PAIRS ? NBW / 2 : 0;
   static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
   // full L2 tiles per filter, then a tail of TB blocks on the 16x16x64 chain when the wave's two
   // filters' tail columns fit its 16 columns (FPW * TC <= 16); otherwise (short trials, e.g.
@@ -442,6 +451,22 @@ __device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
   return (v4i)v;
 }
 
+// Channel-major block pairs (Cfg::PAIRS): lane (cc, k) = (L >> 2, L & 3) of load g reads bytes
+// 16 k .. 16 k + 15 of the pair's 64 bytes of channel row cc + g C / 2; lanes past 2 C read zeros.
+template <class K>
+__device__ __forceinline__ int lane_xoff_pair(int lane, int wave) {
+  if (lane >= 2 * K::C) return (int)0x80000000u;
+  return (lane >> 2) * K::T + 16 * (lane & 3) + 32 * l1_start<K>(wave);
+}
+template <class K>
+__device__ __forceinline__ int pair_off(int i) {  // slot i < 2 NPAIR: pair i >> 1, load i & 1
+  return (i & 1) * (K::C / 2) * K::T + 64 * (i >> 1);
+}
+template <class K>
+__device__ __forceinline__ v4i load_pair(Rsrc r, int xoffp, int i) {
+  return (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xoffp, pair_off<K>(i), MIB_CT_AUX);
+}
+
 // The batch's last trial, channel-major: the one dword of the view that holds the trial's last
 // byte(s) and straddles its end read as zeros (trial_rsrc); the lane holding it reloads those 1-3
 // bytes one at a time (byte loads are range-checked per byte).  Once per launch.
@@ -512,6 +537,50 @@ __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   return (v4i){lo[0], lo[1], hi[0], hi[1]};
 }
 
+// the A fragment of the block staged at stg (two transposed reads)
+__device__ __forceinline__ v4i staged_tr(const int8_t* stg, int lane) {
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 0)));
+  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 1)));
+  return (v4i){lo[0], lo[1], hi[0], hi[1]};
+}
+
+// A pair of blocks (Cfg::PAIRS) into the two staging areas: lane (cc, k) of load g holds channel
+// c = cc + g C / 2, samples 16 k .. 16 k + 15 of the pair, i.e. block k >> 1, half h = k & 1: K-slot
+// row 2 c + h of area k >> 1.  Lanes past the data store their zeros into rows 44 .. 63 of area 0,
+// which only meet zero weights.
+// The batch's last trial (last_trial): the dword of a load straddling the end of the input read as
+// zeros (trial_rsrc); the lane that holds it patches the 1-3 real bytes into its staged row with
+// byte loads and byte stores (once per launch, and kept out of the registers of the common path).
+template <class K>
+__device__ __forceinline__ void stage_pair(v4i ra, v4i rb, int8_t* stg, int lane, int wave, int j, bool last_trial,
+                                           Rsrc rcur) {
+  asm volatile("" : "+v"(lane));  // store addresses recomputed per pair, not hoisted out of the loop
+  const int cc = lane >> 2, k = lane & 3;
+  const bool real = lane < 2 * K::C;
+  const int area = 1024 * (k >> 1);
+  const int wa = real ? area + 16 * stg_pos(2 * cc + (k & 1)) : 16 * lane;
+  const int wb = real ? area + 16 * stg_pos(2 * (cc + K::C / 2) + (k & 1)) : 16 * lane;
+  wave_sync_lds();  // the previous blocks' reads precede these stores
+  *(v4i*)(stg + wa) = ra;
+  *(v4i*)(stg + wb) = rb;
+  if (last_trial) {
+    constexpr int N = K::C * K::T;
+    const int xp = lane_xoff_pair<K>(lane, wave);
+#pragma unroll
+    for (int g = 0; g < 2; g++) {
+      const int o = xp + pair_off<K>(2 * j + g);
+      if (real && o < N && N < o + 16 && ((N - o) & 3)) {
+        const int k0 = (N - o) & ~3;
+        for (int m = 0; o + k0 + m < N; m++)
+          stg[(g ? wb : wa) + k0 + m] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
+      }
+    }
+  }
+  wave_sync_lds();
+}
+
 // Float input, HBM traffic (float input; pmc_traffic.json b22_f32).  Float rows are
 // not 128-byte aligned, so a cache line at a border between two blocks holds bytes of both.  With
 // every wave walking forward, the next wave's first block was requested a trial ahead while this
@@ -534,7 +603,7 @@ __device__ __forceinline__ v4i load_f(Rsrc r, int xoff, int i, int m) {
 }
 
 template <class K>
-__device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R) {
+__device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, int wave = 0) {
   // laundered: otherwise xoff + 16 GS i is hoisted out of the trial loop into a register per slot
   // instead of riding in the loads' immediate offsets
   int xo = R.xoff;
@@ -542,6 +611,17 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R) {
   if constexpr (K::FQ) {  // the first block's four pieces
 #pragma unroll
     for (int m = 0; m < 4; m++) R.pf[m] = load_f<K>(r, xo, R.fq0, m);
+    return;
+  }
+  if constexpr (K::PAIRS) {
+    // the pair offset is recomputed from the lane id each trial (a register across the loop spills)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int xp = lane_xoff_pair<K>(ln, wave);
+#pragma unroll
+    for (int i = 0; i < 2 * K::NPAIR; i++) R.pf[i] = load_pair<K>(r, xp, i);
+#pragma unroll
+    for (int i = 2 * K::NPAIR; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, i);
     return;
   }
 #pragma unroll
@@ -761,6 +841,39 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
   for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
   int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;  // channel-major staging
+  if constexpr (K::PAIRS) {
+    // block pairs: both blocks of pair j are staged at once (two stores into the two areas); the
+    // second block's fragment is read after the first block's MFMAs (registers)
+#pragma unroll
+    for (int j = 0; j < K::NPAIR; j++) {
+      if (2 * j < n) {  // wave-uniform
+        const v4i ra = R.pf[2 * j], rb = R.pf[2 * j + 1];
+        stage_pair<K>(ra, rb, stg, lane, wave, j, last_trial, rcur);
+        const v4i a0 = staged_tr(stg, lane);
+        const int b0 = l1_blk<K>(wave, 2 * j), b1 = l1_blk<K>(wave, 2 * j + 1);
+        if (b0 == K::NB1 - 1) l1_block<K, true>(a0, b0, smem_y1, R, lane);
+        else l1_block<K, false>(a0, b0, smem_y1, R, lane);
+        if (2 * j + 1 < n) {
+          const v4i a1 = staged_tr(stg + 1024, lane);
+          if (b1 == K::NB1 - 1) l1_block<K, true>(a1, b1, smem_y1, R, lane);
+          else l1_block<K, false>(a1, b1, smem_y1, R, lane);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 2 * K::NPAIR; i < K::NBW; i++) {  // an odd last block
+      if (i < n) {
+        const int blk = l1_blk<K>(wave, i);
+        v4i a = R.pf[i];
+        if (last_trial && blk == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
+        a = stage_block<K>(a, stg, lane);
+        if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
+        else l1_block<K, false>(a, blk, smem_y1, R, lane);
+      }
+    }
+    prefetch_l1<K>(rnext, R, lane, wave);
+    return;
+  }
   if constexpr (K::CT && MIB_CT_DBUF) {
     // block i + 1 is staged (store + transposed reads) before block i's MFMAs and requant, so the
     // LDS round trip of the staging overlaps the previous block's work (two staging areas)
@@ -1196,7 +1309,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   R.qy = qy;
   const SmallParams* sp = (const SmallParams*)(smem + K::OFF_SP);
   if ((int)blockIdx.x < B)
-    prefetch_l1<K>(trial_rsrc<K>(x + MIB_TRIAL_OFF(blockIdx.x), MIB_TRIALS_LEFT(blockIdx.x), wave), R);
+    prefetch_l1<K>(trial_rsrc<K>(x + MIB_TRIAL_OFF(blockIdx.x), MIB_TRIALS_LEFT(blockIdx.x), wave), R, lane, wave);
   // The first trial's fragments land before its layer 1 starts, as in k_layer (where loads still
   // in flight at layer 1 gave a rare wrong layer-1 row).  Once per workgroup.
   __builtin_amdgcn_s_waitcnt(0);
@@ -1307,7 +1420,7 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
   __syncthreads();
   if (stage == 1) {  // [T][C] packed (XTRIAL bytes) -> [F1][T_ALIGN]
     const Rsrc rin = trial_rsrc<K>(in, 1, wave);
-    prefetch_l1<K>(rin, R);
+    prefetch_l1<K>(rin, R, lane, wave);
     // All fragment loads land before layer 1 starts.  With them still in flight, this single-
     // workgroup path gave a wrong layer-1 row in ~2 % of calls on gfx950 (tools/stress.py; the
     // batched kernel, whose fragments are loaded a whole trial ahead, showed none in 39 M trials).
