@@ -120,12 +120,24 @@ struct Cfg {
 #ifndef MIB_CT_PAIRS
 #define MIB_CT_PAIRS 0
 #endif
-  // channel-major int8, P == 2, every block prefetched: blocks 2j, 2j + 1 are loaded as a pair, two
-  // loads of C / 2 rows x 64 bytes (layer1, stage_pair); an odd last block alone.  Off: same box
-  // +3.3 % against the double-buffered single blocks (a timing proxy of the load pattern alone had
-  // promised -3.2 %; the pair gives up the staging overlap and its stores scatter)
-  static constexpr bool PAIRS = MIB_CT_PAIRS && CT_ && !FQ_ && P == 2 && PF == NBW && NBW >= 2 && C % 2 == 0;
-  static constexpr int NPAIR = PAIRS ? NBW / 2 : 0;
+#ifndef MIB_CT_QUADS
+#define MIB_CT_QUADS 0
+#endif
+  // Channel-major int8 with every block prefetched: block groups.  The GB blocks of a group cover
+  // 64 samples of every row and are loaded as GL loads of RPL rows x 64 bytes (lane (cc, k): row
+  // cc + g RPL, bytes 16 k), where single-block loads touch every row for 16 (P == 1) or 32 bytes;
+  // a group is staged at once into GB areas (layer1, stage_group).  P == 1 (64 channels): quads,
+  // GL = C / 16 loads of 16 rows.  P == 2: pairs, 2 loads of C / 2 rows.  Both off: same box, pairs
+  // +3.3 % on config B, quads +12.4 % on C and +8.7 % on 64x480 against the double-buffered single
+  // blocks (a group gives up the staging overlap).
+  static constexpr int GB = P == 2 ? 2 : 4;             // blocks per group
+  static constexpr int RPL = P == 2 ? C / 2 : 16;       // rows per group load
+  static constexpr int GL = P == 2 ? 2 : C / 16;        // loads per group
+  static constexpr bool GROUPS = CT_ && !FQ_ && PF == NBW && NBW >= GB &&
+                                 (P == 2 ? (MIB_CT_PAIRS && C % 2 == 0) : (MIB_CT_QUADS && C % 16 == 0));
+  static constexpr int NGRP = GROUPS ? NBW / GB : 0;
+  static constexpr int NGS = NGRP * GL;                  // prefetch slots of the groups
+  static_assert(!GROUPS || NGS + (NBW - NGRP * GB) == PF, "group slots + single slots = prefetched registers");
   static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
   // full L2 tiles per filter, then a tail of TB blocks on the 16x16x64 chain when the wave's two
   // filters' tail columns fit its 16 columns (FPW * TC <= 16); otherwise (short trials, e.g.
@@ -158,7 +170,7 @@ struct Cfg {
 #ifndef MIB_CT_DBUF
 #define MIB_CT_DBUF 1
 #endif
-  static constexpr int STG = MIB_CT_DBUF ? 2048 : 1024;  // two areas: block i + 1 is staged under block i
+  static constexpr int STG = cmax(MIB_CT_DBUF ? 2048 : 1024, 1024 * GB * (GROUPS ? 1 : 0));  // areas of 1 KB
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   // layer 3: tile 1 = the first L3C blocks of both filters side by side (one 16x16x64 MFMA),
   // tile 2 = the L3R outputs past 128, four per column in register 0 only (layer3)
@@ -451,20 +463,20 @@ __device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
   return (v4i)v;
 }
 
-// Channel-major block pairs (Cfg::PAIRS): lane (cc, k) = (L >> 2, L & 3) of load g reads bytes
-// 16 k .. 16 k + 15 of the pair's 64 bytes of channel row cc + g C / 2; lanes past 2 C read zeros.
+// Channel-major block groups (Cfg::GROUPS): lane (cc, k) = (L >> 2, L & 3) of load g reads bytes
+// 16 k .. 16 k + 15 of the group's 64 bytes of channel row cc + g RPL; lanes past 4 RPL read zeros.
 template <class K>
-__device__ __forceinline__ int lane_xoff_pair(int lane, int wave) {
-  if (lane >= 2 * K::C) return (int)0x80000000u;
-  return (lane >> 2) * K::T + 16 * (lane & 3) + 32 * l1_start<K>(wave);
+__device__ __forceinline__ int lane_xoff_grp(int lane, int wave) {
+  if (lane >= 4 * K::RPL) return (int)0x80000000u;
+  return (lane >> 2) * K::T + 16 * (lane & 3) + 16 * K::P * l1_start<K>(wave);
 }
 template <class K>
-__device__ __forceinline__ int pair_off(int i) {  // slot i < 2 NPAIR: pair i >> 1, load i & 1
-  return (i & 1) * (K::C / 2) * K::T + 64 * (i >> 1);
+__device__ __forceinline__ int grp_off(int i) {  // slot i < NGS: group i / GL, load i % GL
+  return (i % K::GL) * K::RPL * K::T + 64 * (i / K::GL);
 }
 template <class K>
-__device__ __forceinline__ v4i load_pair(Rsrc r, int xoffp, int i) {
-  return (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xoffp, pair_off<K>(i), MIB_CT_AUX);
+__device__ __forceinline__ v4i load_grp(Rsrc r, int xoffg, int i) {
+  return (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xoffg, grp_off<K>(i), MIB_CT_AUX);
 }
 
 // The batch's last trial, channel-major: the one dword of the view that holds the trial's last
@@ -546,35 +558,39 @@ __device__ __forceinline__ v4i staged_tr(const int8_t* stg, int lane) {
   return (v4i){lo[0], lo[1], hi[0], hi[1]};
 }
 
-// A pair of blocks (Cfg::PAIRS) into the two staging areas: lane (cc, k) of load g holds channel
-// c = cc + g C / 2, samples 16 k .. 16 k + 15 of the pair, i.e. block k >> 1, half h = k & 1: K-slot
-// row 2 c + h of area k >> 1.  Lanes past the data store their zeros into rows 44 .. 63 of area 0,
-// which only meet zero weights.
+// A block group (Cfg::GROUPS) into the GB staging areas: lane (cc, k) of load g holds channel
+// c = cc + g RPL, samples 16 k .. 16 k + 15 of the group: P == 2: block k >> 1, half k & 1, K-slot row
+// 2 c + (k & 1); P == 1: block k, K-slot row c.  Lanes past the data (P == 2) store their zeros
+// into rows 4 RPL .. 63 of area 0, which only meet zero weights.
 // The batch's last trial (last_trial): the dword of a load straddling the end of the input read as
 // zeros (trial_rsrc); the lane that holds it patches the 1-3 real bytes into its staged row with
-// byte loads and byte stores (once per launch, and kept out of the registers of the common path).
+// byte loads and byte stores (once per launch, and kept out of the registers of the common path:
+// patching the registers pushed the pair build to a spill whose reload drained the prefetch).
 template <class K>
-__device__ __forceinline__ void stage_pair(v4i ra, v4i rb, int8_t* stg, int lane, int wave, int j, bool last_trial,
-                                           Rsrc rcur) {
-  asm volatile("" : "+v"(lane));  // store addresses recomputed per pair, not hoisted out of the loop
+__device__ __forceinline__ void stage_group(const v4i* r, int8_t* stg, int lane, int wave, int q, bool last_trial,
+                                            Rsrc rcur) {
+  asm volatile("" : "+v"(lane));  // store addresses recomputed per group, not hoisted out of the loop
   const int cc = lane >> 2, k = lane & 3;
-  const bool real = lane < 2 * K::C;
-  const int area = 1024 * (k >> 1);
-  const int wa = real ? area + 16 * stg_pos(2 * cc + (k & 1)) : 16 * lane;
-  const int wb = real ? area + 16 * stg_pos(2 * (cc + K::C / 2) + (k & 1)) : 16 * lane;
+  const bool real = lane < 4 * K::RPL;
+  const int area = 1024 * (K::P == 2 ? k >> 1 : k);
   wave_sync_lds();  // the previous blocks' reads precede these stores
-  *(v4i*)(stg + wa) = ra;
-  *(v4i*)(stg + wb) = rb;
+  int w[K::GL];
+#pragma unroll
+  for (int g = 0; g < K::GL; g++) {
+    const int c = cc + g * K::RPL;
+    w[g] = real ? area + 16 * stg_pos(K::P == 2 ? 2 * c + (k & 1) : c) : 16 * lane;
+    *(v4i*)(stg + w[g]) = r[g];
+  }
   if (last_trial) {
     constexpr int N = K::C * K::T;
-    const int xp = lane_xoff_pair<K>(lane, wave);
+    const int xg = lane_xoff_grp<K>(lane, wave);
 #pragma unroll
-    for (int g = 0; g < 2; g++) {
-      const int o = xp + pair_off<K>(2 * j + g);
+    for (int g = 0; g < K::GL; g++) {
+      const int o = xg + grp_off<K>(q * K::GL + g);
       if (real && o < N && N < o + 16 && ((N - o) & 3)) {
         const int k0 = (N - o) & ~3;
         for (int m = 0; o + k0 + m < N; m++)
-          stg[(g ? wb : wa) + k0 + m] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
+          stg[w[g] + k0 + m] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
       }
     }
   }
@@ -613,15 +629,15 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
     for (int m = 0; m < 4; m++) R.pf[m] = load_f<K>(r, xo, R.fq0, m);
     return;
   }
-  if constexpr (K::PAIRS) {
-    // the pair offset is recomputed from the lane id each trial (a register across the loop spills)
+  if constexpr (K::GROUPS) {
+    // the group offset is recomputed from the lane id each trial (a register across the loop spills)
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int xp = lane_xoff_pair<K>(ln, wave);
+    const int xg = lane_xoff_grp<K>(ln, wave);
 #pragma unroll
-    for (int i = 0; i < 2 * K::NPAIR; i++) R.pf[i] = load_pair<K>(r, xp, i);
+    for (int i = 0; i < K::NGS; i++) R.pf[i] = load_grp<K>(r, xg, i);
 #pragma unroll
-    for (int i = 2 * K::NPAIR; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, i);
+    for (int i = K::NGS; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, K::NGRP * K::GB + i - K::NGS);
     return;
   }
 #pragma unroll
@@ -841,30 +857,30 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
   for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
   int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;  // channel-major staging
-  if constexpr (K::PAIRS) {
-    // block pairs: both blocks of pair j are staged at once (two stores into the two areas); the
-    // second block's fragment is read after the first block's MFMAs (registers)
+  if constexpr (K::GROUPS) {
+    // block groups: the GB blocks of group q are staged at once (GL stores into GB areas); each
+    // block's fragment is read just before its MFMAs (registers)
 #pragma unroll
-    for (int j = 0; j < K::NPAIR; j++) {
-      if (2 * j < n) {  // wave-uniform
-        const v4i ra = R.pf[2 * j], rb = R.pf[2 * j + 1];
-        stage_pair<K>(ra, rb, stg, lane, wave, j, last_trial, rcur);
-        const v4i a0 = staged_tr(stg, lane);
-        const int b0 = l1_blk<K>(wave, 2 * j), b1 = l1_blk<K>(wave, 2 * j + 1);
-        if (b0 == K::NB1 - 1) l1_block<K, true>(a0, b0, smem_y1, R, lane);
-        else l1_block<K, false>(a0, b0, smem_y1, R, lane);
-        if (2 * j + 1 < n) {
-          const v4i a1 = staged_tr(stg + 1024, lane);
-          if (b1 == K::NB1 - 1) l1_block<K, true>(a1, b1, smem_y1, R, lane);
-          else l1_block<K, false>(a1, b1, smem_y1, R, lane);
+    for (int q = 0; q < K::NGRP; q++) {
+      if (q * K::GB < n) {  // wave-uniform
+        stage_group<K>(&R.pf[q * K::GL], stg, lane, wave, q, last_trial, rcur);
+#pragma unroll
+        for (int bb = 0; bb < K::GB; bb++) {
+          const int i = q * K::GB + bb;
+          if (i < n) {
+            const v4i a = staged_tr(stg + 1024 * bb, lane);
+            const int blk = l1_blk<K>(wave, i);
+            if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
+            else l1_block<K, false>(a, blk, smem_y1, R, lane);
+          }
         }
       }
     }
 #pragma unroll
-    for (int i = 2 * K::NPAIR; i < K::NBW; i++) {  // an odd last block
+    for (int i = K::NGRP * K::GB; i < K::NBW; i++) {  // the blocks past the last group, one at a time
       if (i < n) {
         const int blk = l1_blk<K>(wave, i);
-        v4i a = R.pf[i];
+        v4i a = R.pf[K::NGS + i - K::NGRP * K::GB];
         if (last_trial && blk == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
         a = stage_block<K>(a, stg, lane);
         if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
