@@ -603,8 +603,9 @@ __device__ __forceinline__ void stage_group(const v4i* r, int8_t* stg, int lane,
 // wave's last block arrived at the end of layer 1, and each such line came from HBM twice (1.23x).
 // MIB_FQ_ALT: odd waves walk their blocks backwards, so both sides of every wave border are read
 // in the same phase of the trial.  MIB_FQ_PF_AT: where the next trial's first block is requested:
-// 1 at the end of layer 1, 2 after layer 2, 3 after layer 3; a later request leaves less time for
-// the line it shares with the block loaded next to leave L2.  Same box: 1.231x -> 1.089x (ALT) ->
+// 1 at the end of layer 1, 2 after layer 2, 3 after layer 3, 4 at the start of its own layer 1 (no
+// trial-ahead request); a later request leaves less time for the line it shares with the block
+// loaded next to leave L2.  Same box: 1.231x -> 1.089x (ALT) ->
 // 1.021x (ALT + PF_AT 2), -6.9 % time (tools/ab.py --f32, profiles/r04_ab.txt).
 #ifndef MIB_FQ_ALT
 #define MIB_FQ_ALT 1
@@ -823,6 +824,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     // trial (R.pf); block i + 1 is loaded while block i is quantised and computed.
     const int n = l1_count<K>(wave);
     int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;
+    if (MIB_FQ_PF_AT == 4) prefetch_l1<K>(rcur, R);  // no trial-ahead request: the first block now
     v4i cur[4] = {R.pf[0], R.pf[1], R.pf[2], R.pf[3]};
     // MIB_FQ_ALT: odd waves walk their blocks backwards (slot n - 1 first), so that both sides of
     // every wave border are read in the same phase of the trial (float input)
