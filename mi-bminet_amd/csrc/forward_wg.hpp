@@ -44,6 +44,7 @@ constexpr int NWAVES = 8;             // waves per workgroup (one trial per work
 constexpr int FPW = F2 / NWAVES;      // layer-2 / layer-3 filters per wave
 constexpr int NTHREADS = 64 * NWAVES;
 constexpr int WPE = 4;                // waves per SIMD (two workgroups per CU)
+constexpr int LDS_WG_MAX = 160 * 1024 / 2;  // LDS per workgroup at two workgroups per CU
 #ifndef MIB_PF_MAX
 #define MIB_PF_MAX 9
 #endif
@@ -133,7 +134,14 @@ struct Cfg {
   static constexpr int GB = P == 2 ? 2 : 4;             // blocks per group
   static constexpr int RPL = P == 2 ? C / 2 : 16;       // rows per group load
   static constexpr int GL = P == 2 ? 2 : C / 16;        // loads per group
-  static constexpr bool GROUPS = CT_ && !FQ_ && PF == NBW && NBW >= GB &&
+  // Channel-major int8 through LDS-DMA (MIB_CT_DMA, layer1): each block's rows go from HBM straight
+  // into an LDS ring with buffer_load_dwordx4 ... lds, a trial ahead, and the A fragments come back
+  // with ds_read_b64_tr_b8: no VGPR round trip, no ds_write (RS ring slots, LDS carve below).
+#ifndef MIB_CT_DMA
+#define MIB_CT_DMA 1
+#endif
+  static constexpr bool DMA = CT_ && !FQ_ && MIB_CT_DMA;
+  static constexpr bool GROUPS = CT_ && !FQ_ && !DMA && PF == NBW && NBW >= GB &&
                                  (P == 2 ? (MIB_CT_PAIRS && C % 2 == 0) : (MIB_CT_QUADS && C % 16 == 0));
   static constexpr int NGRP = GROUPS ? NBW / GB : 0;
   static constexpr int NGS = NGRP * GL;                  // prefetch slots of the groups
@@ -198,8 +206,28 @@ struct Cfg {
   static constexpr int OFF_LT = align16(OFF_SP + (int)sizeof(SmallParams));   // per-lane offsets
   static constexpr int OFF_L45 = OFF_LT + 64 * 48;                            // layer-4/5 lane offsets
   static constexpr int OFF_L2T = OFF_L45 + 64 * 32;                           // tail band fragments
-  static constexpr int OFF_STG = OFF_L2T + (TB > 0 ? NWAVES * 3 * 64 * 16 : 0);   // CT staging
-  static constexpr int LDS = OFF_STG + (CT ? NWAVES * STG : 0);
+  // DMA: the tail band fragments live in VGPRs (12 per lane; the ring frees the 4 per prefetched
+  // block), so that the ring fits two workgroups per CU
+  static constexpr bool L2TV = DMA && TB > 0;
+  static constexpr int OFF_STG = OFF_L2T + (TB > 0 && !L2TV ? NWAVES * 3 * 64 * 16 : 0);  // CT staging / ring
+  // DMA ring: RS slots of 1 KB per wave (one block image each).  Blocks past RS (config C: 9 blocks,
+  // 6 slots) are prefetched into VGPRs (PFV) and stored into slots already consumed.
+  static constexpr int RS = DMA ? cmin(NBW, (LDS_WG_MAX - OFF_STG) / (NWAVES * 1024)) : 0;
+  static constexpr int PFV = DMA ? NBW - RS : PF;       // blocks prefetched into VGPRs
+  // DMA groups (MIB_CT_DMAW): the ring's first NGD * GB blocks are filled as groups of GB blocks
+  // whose rows are read as 64-byte pieces, 4 lanes per row and 16 rows per DMA instruction (GD
+  // instructions of 1 KB per group, in the group's GB slots), instead of 16 or 32 bytes of every
+  // row per instruction (tools/ab.py --ct)
+#ifndef MIB_CT_DMAW
+#define MIB_CT_DMAW 0
+#endif
+  static constexpr bool DW = DMA && (P == 1 ? MIB_CT_DMAW >= 1 : MIB_CT_DMAW >= 2);  // 2: also P == 2
+  static constexpr int GD = (C + 15) / 16;
+  static constexpr int NGD = DW ? RS / GB : 0;
+  static_assert(!DW || GD <= GB, "a group's DMA instructions fit its slots");
+  static constexpr int LDS = OFF_STG + (DMA ? NWAVES * RS * 1024 : CT ? NWAVES * STG : 0);
+  static_assert(!DMA || RS >= 2, "the DMA ring holds at least two blocks per wave");
+  static_assert(!DMA || LDS <= LDS_WG_MAX, "two workgroups per CU");
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
   static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
   static_assert(T64 >= 1, "T >= 64");
@@ -352,8 +380,11 @@ struct Regs {
   v4i a31, a32;            // layer-3 tile-1 / tile-2 band fragments of the wave's filter pair
   float r3, c3;            // layer-3 requant constants (uniform)
   float qs, qy;            // float input's quantisation scale and RN(1 / scale) (K::FQ)
-  v4i pf[K::PF > 0 ? K::PF : 1];  // layer-1 fragments prefetched one trial ahead
+  v4i pf[K::PFV > 0 ? K::PFV : 1];  // layer-1 fragments prefetched one trial ahead (VGPRs)
+  v4i l2t[K::L2TV ? 3 : 1];  // layer-2 tail band fragments of the wave's filter pair (K::L2TV)
   int xoff;                // lane_xoff(lane)
+  int xg[K::DW && K::P == 1 ? 2 : 1];  // DMA groups: lane offsets of the even / odd DMA instructions
+                                       // (dw_lane_off; P == 2: one, the swizzle ignores j)
   int fq0;                 // float input: slot of the wave's first block in walking order (MIB_FQ_ALT)
 };
 
@@ -412,8 +443,20 @@ __device__ __forceinline__ Rsrc trial_rsrc(const int8_t* xt, int trials_left, in
   return __builtin_amdgcn_make_buffer_rsrc((void*)(xt + wb), (short)0, nrec, 0x00020000);
 }
 
+// Physical row of K-slot k in a channel-major block image (see stage_block); its own inverse.
+__device__ __forceinline__ int stg_pos(int k) { return k ^ ((k >> 1) & 8); }
+
 template <class K>
 __device__ __forceinline__ int lane_xoff(int lane, int wave) {
+  if constexpr (K::DMA) {
+    // LDS-DMA ring (layer1): lane L's 16 bytes land in row L of the block image, so lane L loads
+    // K-slot stg_pos(L) (P == 2: channel k >> 1, samples 16 (k & 1) .. +15 of the block; P == 1:
+    // channel k).  Lanes past the rows (C = 22: K-slots 44..63) read zeros without a fetch.
+    const int k = stg_pos(lane);
+    const int c = K::P == 2 ? k >> 1 : k, h = K::P == 2 ? k & 1 : 0;
+    if (c >= K::C) return (int)0x80000000u;
+    return c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h;
+  }
   if constexpr (K::CT) {
     // channel-major: lane (c, h) (P == 2) or c (P == 1) reads 16 samples of channel row c; block
     // slot i adds 16 P i samples.  Lanes past the rows read zeros without a fetch.
@@ -518,7 +561,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 // 16 g + 8 .. 16 g + 15 (tools/tr8_probe.hip checks the form).  Physical row of K-slot
 // k = 16 g + 8 r + q is stg_pos(k) = 16 g + 8 (r ^ (g & 1)) + q: the two groups of a 32-lane half
 // then read different bank halves (conflict-free); stg_pos is its own inverse.
-__device__ __forceinline__ int stg_pos(int k) { return k ^ ((k >> 1) & 8); }
+// (stg_pos is defined above lane_xoff, whose DMA offsets use it)
 
 #ifndef MIB_TR8_QSEL
 #define MIB_TR8_QSEL 0
@@ -531,7 +574,9 @@ __device__ __forceinline__ int stg_read_off(int lane, int r) {
   return 16 * stg_pos(16 * g + 8 * r + q) + 8 * p;
 }
 
-template <class K>
+// IDENT: the lane already holds K-slot stg_pos(lane) (the DMA ring's lane offsets), so its row goes
+// to row lane of the image
+template <class K, bool IDENT = false>
 __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   typedef int v2i __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) v2i lds_v2i;
@@ -541,7 +586,7 @@ __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   // which needs no VGPR -> LDS transfer, could at most save); the loaded data is kept live
   asm volatile("" ::"v"(raw));
 #else
-  *(v4i*)(stg + 16 * stg_pos(lane)) = raw;
+  *(v4i*)(stg + 16 * (IDENT ? lane : stg_pos(lane))) = raw;
 #endif
   wave_sync_lds();
   const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 0)));
@@ -555,6 +600,57 @@ __device__ __forceinline__ v4i staged_tr(const int8_t* stg, int lane) {
   typedef __attribute__((address_space(3))) v2i lds_v2i;
   const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 0)));
   const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 1)));
+  return (v4i){lo[0], lo[1], hi[0], hi[1]};
+}
+
+// LDS-DMA (channel-major ring, K::DMA): buffer_load_dwordx4 ... lds writes lane L's 16 bytes from
+// voff + soff of the buffer to LDS byte m0 + 16 L (lane-linear; byte-unaligned sources and a dword
+// straddling num_records, which lands as zeros, were checked on gfx950 by tools/tr8_probe.hip).
+// Inline asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: with the builtin the compiler makes
+// every __syncthreads() wait for the DMA (s_waitcnt vmcnt(0) before s_barrier), which would drain
+// the trial-ahead fill at barrier A.  So the waits are explicit: layer1 waits vmcnt(0) before it
+// reads the ring, and the fill waits lgkmcnt(0) (the ring's reads done) before it is issued.  The
+// compiler's own vmcnt counts stay safe: a wait for one of its loads only ever waits longer when
+// DMA loads it does not know about are in flight (in-order completion).
+__device__ __forceinline__ unsigned lds_addr(const int8_t* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) int8_t*)p;
+}
+__device__ __forceinline__ void dma_b128(Rsrc r, int voff, int soff, unsigned lds) {
+  asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+               :: "v"(voff), "s"(r), "s"(soff), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");  // m0: no other user in these kernels (tests/test_mfma_lint.py)
+}
+
+// DMA groups (K::DW).  Instruction j of a group fills KB j of the group's GB slots: lane L = (r, k')
+// = (L >> 2, L & 3) writes slot 4 r + k' with piece k' ^ dw_swz(c) of channel row c = 16 j + r, a
+// piece being 16 bytes of the group's 64 bytes of the row (P == 2: block k >> 1, half k & 1;
+// P == 1: block k).  The XOR swizzle makes the transposed reads conflict-free: a 32-lane half of
+// ds_read_b64_tr_b8 reads 16 channels whose 16-byte pieces then fall on 64 distinct banks.
+template <class K>
+__device__ __forceinline__ int dw_swz(int c) {
+  return K::P == 2 ? (c >> 2) & 2 : ((c >> 2) & 1) | ((c >> 3) & 2);
+}
+// lane offset of instruction j (the instruction adds 16 j T + 64 q through soffset; only j & 1
+// matters); rows past C land past the view and read zeros
+template <class K>
+__device__ __forceinline__ int dw_lane_off(int lane, int wave, int j) {
+  const int r = lane >> 2, kq = lane & 3;
+  return r * K::T + 16 * (kq ^ dw_swz<K>(16 * j + r)) + 16 * K::P * l1_start<K>(wave);
+}
+// byte offset in the group's slots of lane (i, g)'s transposed read rr of the group's block b
+template <class K>
+__device__ __forceinline__ int dw_read_off(int lane, int rr, int b) {
+  const int i = lane & 15, g = lane >> 4, q = i >> 1, p = i & 1;
+  const int kk = 16 * g + 8 * rr + q;
+  const int c = K::P == 2 ? kk >> 1 : kk, h = K::P == 2 ? kk & 1 : 0;
+  const int piece = K::P == 2 ? 2 * b + h : b;
+  return 1024 * (c >> 4) + 64 * (c & 15) + 16 * (piece ^ dw_swz<K>(c)) + 8 * p;
+}
+template <class K>
+__device__ __forceinline__ v4i dw_tr(const int8_t* grp, int lane, int b) {
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(grp + dw_read_off<K>(lane, 0, b)));
+  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(grp + dw_read_off<K>(lane, 1, b)));
   return (v4i){lo[0], lo[1], hi[0], hi[1]};
 }
 
@@ -620,11 +716,32 @@ __device__ __forceinline__ v4i load_f(Rsrc r, int xoff, int i, int m) {
 }
 
 template <class K>
-__device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, int wave = 0) {
+__device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, int wave = 0,
+                                            int8_t* ring = nullptr) {
   // laundered: otherwise xoff + 16 GS i is hoisted out of the trial loop into a register per slot
   // instead of riding in the loads' immediate offsets
   int xo = R.xoff;
   asm volatile("" : "+v"(xo));
+  if constexpr (K::DMA) {
+    // ring slots 0 .. RS - 1 by LDS-DMA, the rest into VGPRs.  The ring's transposed reads of the
+    // trial just computed have returned (their MFMAs consumed them); the wait makes that explicit
+    // for the hardware, which would otherwise let a DMA write race a read still queued.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const unsigned rb = lds_addr(ring);
+#pragma unroll
+    for (int q = 0; q < K::NGD; q++)
+#pragma unroll
+      for (int j = 0; j < K::GD; j++) {
+        int xg = R.xg[K::P == 1 ? j & 1 : 0];
+        asm volatile("" : "+v"(xg));
+        dma_b128(r, xg, 16 * j * K::T + 64 * q, rb + 1024 * (K::GB * q + j));
+      }
+#pragma unroll
+    for (int i = K::NGD * K::GB; i < K::RS; i++) dma_b128(r, xo, 16 * K::P * i, rb + 1024 * i);
+#pragma unroll
+    for (int i = 0; i < K::PFV; i++) R.pf[i] = load_a<K>(r, xo, K::RS + i);
+    return;
+  }
   if constexpr (K::FQ) {  // the first block's four pieces
 #pragma unroll
     for (int m = 0; m < 4; m++) R.pf[m] = load_f<K>(r, xo, R.fq0, m);
@@ -652,6 +769,10 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   for (int t = 0; t < K::P; t++) {
     L1Tile& T = R.tile(t);
     R.xoff = lane_xoff<K>(lane, wave);
+    if constexpr (K::DW) {
+      R.xg[0] = dw_lane_off<K>(lane, wave, 0);
+      if constexpr (K::P == 1) R.xg[K::P == 1 ? 1 : 0] = dw_lane_off<K>(lane, wave, 1);
+    }
     T.wf = K::CT ? prm->l1_wfrag_ct[t][lane] : prm->l1_wfrag[t][lane];
     T.ci = prm->l1_cinit[t][lane & 15];
     T.rr = prm->l1_r[t][lane & 15];
@@ -683,7 +804,10 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   for (int i = tid; i < (int)(sizeof(SmallParams) / 16); i += NTHREADS) dst[i] = src[i];
   if (tid < 64) ((LaneTab*)(smem + K::OFF_LT))[tid] = build_lane_tab<K>(tid);
   if (tid < 64) ((L45Tab*)(smem + K::OFF_L45))[tid] = build_l45_tab<K>(tid);
-  if constexpr (K::TB > 0) {
+  if constexpr (K::L2TV) {
+#pragma unroll
+    for (int s = 0; s < 3; s++) R.l2t[s] = K::L2NAT ? prm->l2t_afrag_n[wave][s][lane] : prm->l2t_afrag[wave][s][lane];
+  } else if constexpr (K::TB > 0) {
     const v4i* t = K::L2NAT ? &prm->l2t_afrag_n[0][0][0] : &prm->l2t_afrag[0][0][0];
     v4i* d = (v4i*)(smem + K::OFF_L2T);
     for (int i = tid; i < NWAVES * 3 * 64; i += NTHREADS) d[i] = t[i];
@@ -692,6 +816,12 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   // ([0,8) and [8+T8, Y2ROW)) and the zero row are never rewritten
   v4i* z = (v4i*)smem;
   for (int i = tid; i < K::OFF_SP / 16; i += NTHREADS) z[i] = (v4i){0, 0, 0, 0};
+  if constexpr (K::DMA) {
+    // the wave's own ring slots (rows that no lane fills, C = 22: K-slots 44..63, stay zero either
+    // way); the wave's first fill waits for these stores (prefetch_l1)
+    v4i* rz = (v4i*)(smem + K::OFF_STG + wave * K::RS * 1024);
+    for (int i = lane; i < K::RS * 64; i += 64) rz[i] = (v4i){0, 0, 0, 0};
+  }
 }
 
 // ---- layer 1 ---------------------------------------------------------------------------------
@@ -853,6 +983,74 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     if (MIB_FQ_PF_AT == 1) prefetch_l1<K>(rnext, R);  // else from the trial loop (k_forward)
     return;
   }
+  if constexpr (K::DMA) {
+    // Channel-major through the LDS-DMA ring: slots 0 .. RS - 1 hold blocks 0 .. RS - 1, filled a
+    // trial ahead (prefetch_l1); blocks past RS come from VGPRs and are stored into slots already
+    // consumed.  Block i + 1's fragment is read before block i's MFMAs and requant.
+    const int n = l1_count<K>(wave);
+    int8_t* ring = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::RS * 1024;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this trial's fill has landed
+    if (last_trial) {
+      // the batch's last trial: its view ends at its last byte, so the one dword straddling that
+      // end landed as zeros; the lane holding it patches the 1-3 real bytes in (byte loads and
+      // stores, once per launch; blocks past RS are patched in registers by ct_tail)
+      constexpr int N = K::C * K::T;
+#pragma unroll
+      for (int q = 0; q < K::NGD; q++)
+#pragma unroll
+        for (int j = 0; j < K::GD; j++) {
+          const int o = R.xg[K::P == 1 ? j & 1 : 0] + 16 * j * K::T + 64 * q;
+          if (o < N && N < o + 16 && ((N - o) & 3)) {
+            const int k0 = (N - o) & ~3;
+            for (int m = 0; o + k0 + m < N; m++)
+              ring[1024 * (K::GB * q + j) + 16 * lane + k0 + m] =
+                  (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
+          }
+        }
+#pragma unroll
+      for (int i = K::NGD * K::GB; i < K::RS; i++) {
+        const int o = R.xoff + 16 * K::P * i;
+        if (i < n && l1_blk<K>(wave, i) == K::NB1 - 1 && o < N && N < o + 16 && ((N - o) & 3)) {
+          const int k0 = (N - o) & ~3;
+          for (int m = 0; o + k0 + m < N; m++)
+            ring[1024 * i + 16 * lane + k0 + m] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
+        }
+      }
+      wave_sync_lds();
+    }
+    auto ring_tr = [&](int i) -> v4i {  // block i < RS
+      if (i < K::NGD * K::GB) {
+        int ln = lane;  // read offsets recomputed per block: hoisted, they hold 2 GB registers
+        asm volatile("" : "+v"(ln));
+        return dw_tr<K>(ring + 1024 * K::GB * (i / K::GB), ln, i % K::GB);
+      }
+      return staged_tr(ring + 1024 * i, lane);
+    };
+    v4i an = ring_tr(0);
+#pragma unroll
+    for (int i = 0; i < K::NBW; i++) {
+      if (i < n) {  // wave-uniform
+        const int blk = l1_blk<K>(wave, i);
+        const v4i a = an;
+        if (i + 1 < n) {
+          if (i + 1 < K::RS) {
+            an = ring_tr(i + 1);
+          } else {
+            v4i raw = R.pf[i + 1 >= K::RS ? i + 1 - K::RS : 0];
+            if (last_trial && l1_blk<K>(wave, i + 1) == K::NB1 - 1) raw = ct_tail<K>(raw, rcur, R.xoff + 16 * K::P * (i + 1));
+            an = stage_block<K, true>(raw, ring + 1024 * (i + 1 - K::RS), lane);
+          }
+        }
+        if (blk == K::NB1 - 1) {
+          l1_block<K, true>(a, blk, smem_y1, R, lane);
+        } else {
+          l1_block<K, false>(a, blk, smem_y1, R, lane);
+        }
+      }
+    }
+    prefetch_l1<K>(rnext, R, lane, wave, ring);
+    return;
+  }
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
   v4i xa[NX > 0 ? NX : 1];
 #pragma unroll
@@ -994,7 +1192,7 @@ __device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, fl
 // pool window g >> 1; lanes g and g ^ 1 meet by v_permlane16_swap (layer2_tail_out).
 template <class K>
 __device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const SmallParams* sp, const LaneTab& T,
-                                                int wave, int lane) {
+                                                const Regs<K>& R, int wave, int lane) {
   const v4i* tA = (const v4i*)(smem_y1 - K::OFF_Y1 + K::OFF_L2T) + wave * 3 * 64 + lane;
   const int8_t* pb = smem_y1 + wave * FPW * K::Y1ROW;
   v4i bv[3], a[3];
@@ -1003,7 +1201,7 @@ __device__ __forceinline__ v4i layer2_tail_mfma(const int8_t* smem_y1, const Sma
     const long* q = (const long*)(pb + T.tb[st]);  // 8-byte aligned
     const long lo = q[0], hi = q[1];
     bv[st][0] = (int)lo; bv[st][1] = (int)(lo >> 32); bv[st][2] = (int)hi; bv[st][3] = (int)(hi >> 32);
-    a[st] = tA[st * 64];
+    a[st] = K::L2TV ? R.l2t[st] : tA[st * 64];
   }
   const int c0 = K::RB ? PBIAS_TAIL : 0;
   v4i acc = {c0, c0, c0, c0};
@@ -1105,7 +1303,7 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 #if MIB_PRIO_TAIL
     __builtin_amdgcn_s_setprio(MIB_PRIO_TAIL);  // knob (A/B)
 #endif
-    const v4i tacc = layer2_tail_mfma<K>(smem_y1, sp, T, wave, lane);
+    const v4i tacc = layer2_tail_mfma<K>(smem_y1, sp, T, R, wave, lane);
     layer2_tail_out<K>(tacc, smem_y2, sp, T, wave);
   }
   // Sensitivity diagnostics (tools/ab.py builds only): extra independent work per wave and trial
@@ -1327,7 +1525,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   R.qy = qy;
   const SmallParams* sp = (const SmallParams*)(smem + K::OFF_SP);
   if ((int)blockIdx.x < B)
-    prefetch_l1<K>(trial_rsrc<K>(x + MIB_TRIAL_OFF(blockIdx.x), MIB_TRIALS_LEFT(blockIdx.x), wave), R, lane, wave);
+    prefetch_l1<K>(trial_rsrc<K>(x + MIB_TRIAL_OFF(blockIdx.x), MIB_TRIALS_LEFT(blockIdx.x), wave), R, lane, wave,
+                   smem + K::OFF_STG + wave * K::RS * 1024);
   // The first trial's fragments land before its layer 1 starts, as in k_layer (where loads still
   // in flight at layer 1 gave a rare wrong layer-1 row).  Once per workgroup.
   __builtin_amdgcn_s_waitcnt(0);
