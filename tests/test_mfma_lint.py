@@ -100,6 +100,62 @@ def test_no_inline_asm_hazard_next_to_mfma(tmp_path):
     assert not hazards, "\n".join(hazards)
 
 
+@pytest.fixture(scope="module")
+def device_asm(tmp_path_factory):
+    """gfx950 assembly of the library's kernels (one compile per module)."""
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not installed")
+    asm = tmp_path_factory.mktemp("asm") / "mibminet.s"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wno-unused-function",
+                    "-mllvm", "-disable-promote-alloca-to-lds", "--cuda-device-only", "-S", "-o", str(asm),
+                    os.path.join(ROOT, "mi-bminet_amd", "csrc", "mibminet.hip")],
+                   check=True, capture_output=True)
+    return asm
+
+
+def _functions(asm):
+    import re
+    funcs, name = {}, None
+    for line in open(asm):
+        m = re.match(r"^(_Z\w+):", line)
+        if m:
+            name = m.group(1)
+            funcs[name] = []
+        elif name:
+            funcs[name].append(line.strip())
+    return funcs
+
+
+def test_trial_loop_barriers_do_not_drain_prefetch(device_asm):
+    """Every k_forward keeps its next-trial loads in flight across the trial loop's barriers: no
+    s_barrier but the one before the loop follows an s_waitcnt on vmcnt.  The channel-major LDS-DMA
+    fill is inline asm for this reason: with __builtin_amdgcn_raw_ptr_buffer_load_lds
+    the compiler puts vmcnt(0) before every __syncthreads().  The DMA instructions set m0 themselves,
+    and nothing else in these kernels touches m0."""
+    funcs = {n: ls for n, ls in _functions(device_asm).items() if "k_forward" in n}
+    assert len(funcs) == 36
+    n_dma = 0
+    for name, lines in funcs.items():
+        barriers = [i for i, l in enumerate(lines) if l.startswith("s_barrier")]
+        assert len(barriers) >= 3, name
+        for i in barriers[1:]:
+            waits = [l for l in lines[max(0, i - 4):i] if l.startswith("s_waitcnt")]
+            assert not any("vmcnt" in w for w in waits), (name, lines[i - 4:i + 1])
+        in_asm = False
+        for i, l in enumerate(lines):
+            if l.startswith(";;#ASMSTART"):
+                in_asm = True
+            elif l.startswith(";;#ASMEND"):
+                in_asm = False
+            elif "m0" in l.split(";")[0].replace(",", " ").split():
+                assert in_asm and l.startswith("s_mov_b32 m0") and " lds" in lines[i + 1], (name, l)
+        ct_int8 = "ELb1ELb0EEEE" in name  # Cfg<..., CT = true, FQ = false>
+        dma = sum(1 for l in lines if l.startswith("buffer_load_dwordx4") and l.endswith(" lds"))
+        assert (dma > 0) == ct_int8, (name, dma)
+        n_dma += dma > 0
+    assert n_dma == 12
+
+
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
 def test_layer1_cinit_not_written_near_loads(tmp_path):
     """The round-1 layer-1 fault's remaining candidate: an MFMA C-init written by a
