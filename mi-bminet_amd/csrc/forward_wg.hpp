@@ -140,7 +140,9 @@ struct Cfg {
 #ifndef MIB_CT_DMA
 #define MIB_CT_DMA 1
 #endif
-  static constexpr bool DMA = CT_ && !FQ_ && MIB_CT_DMA;
+  // 1: P == 2 (22 channels) only; 2: also P == 1 (64 channels), where 64 rows of 16 bytes per DMA
+  // instruction measured +50 % on config C (LDS-DMA handles scattered rows far worse than VGPR loads)
+  static constexpr bool DMA = CT_ && !FQ_ && (P == 2 ? MIB_CT_DMA >= 1 : MIB_CT_DMA >= 2);
   static constexpr bool GROUPS = CT_ && !FQ_ && !DMA && PF == NBW && NBW >= GB &&
                                  (P == 2 ? (MIB_CT_PAIRS && C % 2 == 0) : (MIB_CT_QUADS && C % 16 == 0));
   static constexpr int NGRP = GROUPS ? NBW / GB : 0;
@@ -702,12 +704,14 @@ __device__ __forceinline__ void stage_group(const v4i* r, int8_t* stg, int lane,
 // 1 at the end of layer 1, 2 after layer 2, 3 after layer 3, 4 at the start of its own layer 1 (no
 // trial-ahead request); a later request leaves less time for the line it shares with the block
 // loaded next to leave L2.  Same box: 1.231x -> 1.089x (ALT) ->
-// 1.021x (ALT + PF_AT 2), -6.9 % time (tools/ab.py --f32, profiles/r04_ab.txt).
+// 1.021x (ALT + PF_AT 2), -6.9 % time (tools/ab.py --f32, profiles/r04_ab.txt).  PF_AT 4: the
+// same 1.022x and another -1.3 % (9 interleaved rounds): the other waves cover the first block's
+// latency, and the wave's registers stay free through layers 2-5.
 #ifndef MIB_FQ_ALT
 #define MIB_FQ_ALT 1
 #endif
 #ifndef MIB_FQ_PF_AT
-#define MIB_FQ_PF_AT 2
+#define MIB_FQ_PF_AT 4
 #endif
 // float input (K::FQ): 16-byte piece m of the lane's 64 bytes of block slot i
 template <class K>
@@ -736,8 +740,10 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
         asm volatile("" : "+v"(xg));
         dma_b128(r, xg, 16 * j * K::T + 64 * q, rb + 1024 * (K::GB * q + j));
       }
+    const int n = l1_count<K>(wave);  // slots past the wave's blocks stay unfilled (wave-uniform)
 #pragma unroll
-    for (int i = K::NGD * K::GB; i < K::RS; i++) dma_b128(r, xo, 16 * K::P * i, rb + 1024 * i);
+    for (int i = K::NGD * K::GB; i < K::RS; i++)
+      if (i < n) dma_b128(r, xo, 16 * K::P * i, rb + 1024 * i);
 #pragma unroll
     for (int i = 0; i < K::PFV; i++) R.pf[i] = load_a<K>(r, xo, K::RS + i);
     return;
@@ -989,7 +995,11 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     // consumed.  Block i + 1's fragment is read before block i's MFMAs and requant.
     const int n = l1_count<K>(wave);
     int8_t* ring = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::RS * 1024;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this trial's fill has landed
+    // this trial's fill has landed.  Issued after it: the PFV VGPR loads and, on the last wave, the
+    // previous trial's logits store, which need not complete (a vmcnt(0) here waited for that
+    // store's write acknowledgement on the critical last wave: +1,200 cycles per trial)
+    if (wave == NWAVES - 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(K::PFV + 1) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(K::PFV) : "memory");
     if (last_trial) {
       // the batch's last trial: its view ends at its last byte, so the one dword straddling that
       // end landed as zeros; the lane holding it patches the 1-3 real bytes in (byte loads and

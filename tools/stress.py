@@ -9,7 +9,7 @@ outputs that differ from the expected ones.
      launch maps different trials to different workgroups and prefetch slots, and is compared
      with the oracle's logits permuted the same way.
 
-    python tools/stress.py [--lib path] [--n1 2000] [--n2 200] [--nb 8] [--B 65536] [--layout ct]
+    python tools/stress.py [--lib path] [--n1 2000] [--n2 200] [--nb 8] [--B 65536] [--layout ct] [--cfg c64]
 
   --layout ct stresses net_model_compute_batch_ct instead: the batches are channel-major
   [B][C][T] (the oracle gets the same trials transposed).  --layout f32 stresses
@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--B", type=int, default=65536)
     ap.add_argument("--nb", type=int, default=8, help="distinct input batches per parameter mode")
     ap.add_argument("--layout", default="tc", choices=("tc", "ct", "f32"))
+    ap.add_argument("--cfg", default="b22", choices=("b22", "c64", "p64"), help="geometry of the batch stress")
     ap.add_argument("--variants", default="canonical",
                     help="comma list of build variants to stress: canonical, plain_bn, clip_balanced")
     a = ap.parse_args()
@@ -62,8 +63,9 @@ def main():
 
     modes = [(v, st) for v in a.variants.split(",") for st in (True, False)]
     for variant, stress in modes:
+        gC, gT = {"b22": (22, 1125), "c64": (64, 1000), "p64": (64, 480)}[a.cfg]
         ps = ParamSet.synthetic(seed=7, stress=stress, reorder_bn=variant != "plain_bn",
-                                clip_balanced=variant == "clip_balanced")
+                                clip_balanced=variant == "clip_balanced", C=gC, T=gT)
         lib.params_load(ps)
         stride = lib.trial_stride()
         g = torch.Generator(device="cuda:0").manual_seed(11 + stress)
@@ -114,7 +116,7 @@ def main():
                 if bad2 <= 5:
                     rows = torch.nonzero(bad).flatten()[:4].tolist()
                     print(f"batch launch {i}: {nb} trials differ, first {rows}", flush=True)
-        print(f"batch ({a.layout}, {variant}, stress={stress}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
+        print(f"batch ({a.layout}, {a.cfg}, {variant}, stress={stress}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
               f"{a.nb * a.B} distinct ({time.time() - t0:.1f} s)", flush=True)
 
 if __name__ == "__main__":
