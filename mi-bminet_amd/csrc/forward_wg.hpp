@@ -180,7 +180,16 @@ struct Cfg {
 #ifndef MIB_CT_DBUF
 #define MIB_CT_DBUF 1
 #endif
-  static constexpr int STG = cmax(MIB_CT_DBUF ? 2048 : 1024, 1024 * GB * (GROUPS ? 1 : 0));  // areas of 1 KB
+  // Channel-major int8, 64 channels, VGPR path (MIB_CT_QL): quads of 4 blocks loaded as 4 loads of
+  // 16 rows x 64 bytes (the DMA groups' lane offsets), stored lane-linearly (4 ds_write_b128 at
+  // 1 KB + 16 lane) into a 4 KB quad area and read with the groups' swizzled transposed reads
+  // (dw_tr); the blocks past the quads go through the single-block staging (1 KB area at 4 KB).
+#ifndef MIB_CT_QL
+#define MIB_CT_QL 0
+#endif
+  static constexpr bool QL = CT_ && !FQ_ && !DMA && !GROUPS && MIB_CT_QL && C == 64 && PF == NBW && NBW >= 4;
+  static constexpr int NQL = QL ? NBW / 4 : 0;          // quads (prefetch slots 4 q + j: load j of quad q)
+  static constexpr int STG = QL ? 5120 : cmax(MIB_CT_DBUF ? 2048 : 1024, 1024 * GB * (GROUPS ? 1 : 0));  // areas of 1 KB
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   // layer 3: tile 1 = the first L3C blocks of both filters side by side (one 16x16x64 MFMA),
   // tile 2 = the L3R outputs past 128, four per column in register 0 only (layer3)
@@ -222,6 +231,9 @@ struct Cfg {
   // row per instruction (tools/ab.py --ct)
 #ifndef MIB_CT_DMAW
 #define MIB_CT_DMAW 0
+#endif
+#ifndef MIB_CT_LA
+#define MIB_CT_LA 1  // DMA ring: blocks of lookahead of the transposed reads (layer1)
 #endif
   static constexpr bool DW = DMA && (P == 1 ? MIB_CT_DMAW >= 1 : MIB_CT_DMAW >= 2);  // 2: also P == 2
   static constexpr int GD = (C + 15) / 16;
@@ -385,7 +397,7 @@ struct Regs {
   v4i pf[K::PFV > 0 ? K::PFV : 1];  // layer-1 fragments prefetched one trial ahead (VGPRs)
   v4i l2t[K::L2TV ? 3 : 1];  // layer-2 tail band fragments of the wave's filter pair (K::L2TV)
   int xoff;                // lane_xoff(lane)
-  int xg[K::DW && K::P == 1 ? 2 : 1];  // DMA groups: lane offsets of the even / odd DMA instructions
+  int xg[(K::DW || K::QL) && K::P == 1 ? 2 : 1];  // DMA groups: lane offsets of the even / odd DMA instructions
                                        // (dw_lane_off; P == 2: one, the swizzle ignores j)
   int fq0;                 // float input: slot of the wave's first block in walking order (MIB_FQ_ALT)
 };
@@ -753,6 +765,19 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
     for (int m = 0; m < 4; m++) R.pf[m] = load_f<K>(r, xo, R.fq0, m);
     return;
   }
+  if constexpr (K::QL) {
+#pragma unroll
+    for (int q = 0; q < K::NQL; q++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        int xg = R.xg[j & 1];
+        asm volatile("" : "+v"(xg));
+        R.pf[4 * q + j] = (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xg, 16 * j * K::T + 64 * q, MIB_CT_AUX);
+      }
+#pragma unroll
+    for (int i = 4 * K::NQL; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, i);
+    return;
+  }
   if constexpr (K::GROUPS) {
     // the group offset is recomputed from the lane id each trial (a register across the loop spills)
     int ln = lane;
@@ -775,7 +800,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   for (int t = 0; t < K::P; t++) {
     L1Tile& T = R.tile(t);
     R.xoff = lane_xoff<K>(lane, wave);
-    if constexpr (K::DW) {
+    if constexpr (K::DW || K::QL) {
       R.xg[0] = dw_lane_off<K>(lane, wave, 0);
       if constexpr (K::P == 1) R.xg[K::P == 1 ? 1 : 0] = dw_lane_off<K>(lane, wave, 1);
     }
@@ -1036,21 +1061,26 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
       }
       return staged_tr(ring + 1024 * i, lane);
     };
-    v4i an = ring_tr(0);
+    auto frag = [&](int i) -> v4i {  // block i's A fragment
+      if (i < K::RS) return ring_tr(i);
+      v4i raw = R.pf[i >= K::RS ? i - K::RS : 0];
+      if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) raw = ct_tail<K>(raw, rcur, R.xoff + 16 * K::P * i);
+      return stage_block<K, true>(raw, ring + 1024 * (i - K::RS), lane);
+    };
+    // fragments are read MIB_CT_LA blocks ahead of their MFMAs (a block past RS is stored into slot
+    // i - RS, whose block was read LA or more iterations earlier: RS >= LA)
+    constexpr int LA = MIB_CT_LA;
+    static_assert(K::RS >= LA, "ring slots cover the lookahead");
+    v4i fr[LA];
+#pragma unroll
+    for (int j = 0; j < LA; j++)
+      if (j < n) fr[j] = frag(j);
 #pragma unroll
     for (int i = 0; i < K::NBW; i++) {
       if (i < n) {  // wave-uniform
         const int blk = l1_blk<K>(wave, i);
-        const v4i a = an;
-        if (i + 1 < n) {
-          if (i + 1 < K::RS) {
-            an = ring_tr(i + 1);
-          } else {
-            v4i raw = R.pf[i + 1 >= K::RS ? i + 1 - K::RS : 0];
-            if (last_trial && l1_blk<K>(wave, i + 1) == K::NB1 - 1) raw = ct_tail<K>(raw, rcur, R.xoff + 16 * K::P * (i + 1));
-            an = stage_block<K, true>(raw, ring + 1024 * (i + 1 - K::RS), lane);
-          }
-        }
+        const v4i a = fr[i % LA];
+        if (i + LA < n) fr[i % LA] = frag(i + LA);
         if (blk == K::NB1 - 1) {
           l1_block<K, true>(a, blk, smem_y1, R, lane);
         } else {
@@ -1067,6 +1097,58 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
   for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
   int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;  // channel-major staging
+  if constexpr (K::QL) {
+    // quads: quad q's 4 loads are stored lane-linearly into the quad area when its first block's
+    // fragment is read, MIB_CT_LA blocks ahead; the previous quad's reads were issued before (the
+    // wave's LDS accesses execute in order)
+    auto store_quad = [&](int q) {
+      wave_sync_lds();
+#pragma unroll
+      for (int j = 0; j < 4; j++) *(v4i*)(stg + 1024 * j + 16 * lane) = R.pf[4 * q + j];
+      if (last_trial) {  // the batch's last trial: its straddling dword read as zeros (trial_rsrc)
+        constexpr int N = K::C * K::T;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const int o = R.xg[j & 1] + 16 * j * K::T + 64 * q;
+          if (o < N && N < o + 16 && ((N - o) & 3)) {
+            const int k0 = (N - o) & ~3;
+            for (int m = 0; o + k0 + m < N; m++)
+              stg[1024 * j + 16 * lane + k0 + m] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
+          }
+        }
+      }
+      wave_sync_lds();
+    };
+    auto frag = [&](int i) -> v4i {
+      if (i < 4 * K::NQL) {
+        if (i % 4 == 0) store_quad(i / 4);
+        int ln = lane;  // read offsets recomputed per block (hoisted, they hold 8 registers)
+        asm volatile("" : "+v"(ln));
+        return dw_tr<K>(stg, ln, i % 4);
+      }
+      v4i raw = R.pf[i < K::PF ? i : 0];
+      if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) raw = ct_tail<K>(raw, rcur, R.xoff + 16 * K::P * i);
+      return stage_block<K>(raw, stg + 4096, lane);
+    };
+    constexpr int LA = MIB_CT_LA;
+    static_assert(LA >= 1 && LA <= 4, "a quad's reads precede the next quad's stores");
+    v4i fr[LA];
+#pragma unroll
+    for (int j = 0; j < LA; j++)
+      if (j < n) fr[j] = frag(j);
+#pragma unroll
+    for (int i = 0; i < K::NBW; i++) {
+      if (i < n) {  // wave-uniform
+        const int blk = l1_blk<K>(wave, i);
+        const v4i a = fr[i % LA];
+        if (i + LA < n) fr[i % LA] = frag(i + LA);
+        if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
+        else l1_block<K, false>(a, blk, smem_y1, R, lane);
+      }
+    }
+    prefetch_l1<K>(rnext, R, lane, wave);
+    return;
+  }
   if constexpr (K::GROUPS) {
     // block groups: the GB blocks of group q are staged at once (GL stores into GB areas); each
     // block's fragment is read just before its MFMAs (registers)
@@ -1621,6 +1703,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
       MIB_STAMP(6)
     }
   }
+  // the last fill (of an empty view past the batch) writes LDS: it lands before the wave ends
+  if constexpr (K::DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   MIB_STAMP_FLUSH(tid == 0, 0)
   MIB_STAMP_FLUSH(tid == 64 * (NWAVES - 1), 1)
   MIB_CLOCK_FLUSH
