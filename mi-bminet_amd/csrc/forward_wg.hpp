@@ -75,6 +75,11 @@ constexpr int PRIO_L1 = MIB_PRIO_L1, PRIO_L45 = MIB_PRIO_L45;
 #ifndef MIB_W45
 #define MIB_W45 4
 #endif
+template <bool V>
+struct BoolC {
+  static constexpr bool value = V;
+};
+
 struct L1Split {
   int cm, rm, cl;
 };
@@ -234,6 +239,9 @@ struct Cfg {
 #endif
 #ifndef MIB_CT_LA
 #define MIB_CT_LA 1  // DMA ring: blocks of lookahead of the transposed reads (layer1)
+#endif
+#ifndef MIB_CT_FULL
+#define MIB_CT_FULL 1  // DMA ring: branch-free layer 1 for the waves with all NBW blocks (layer1)
 #endif
   static constexpr bool DW = DMA && (P == 1 ? MIB_CT_DMAW >= 1 : MIB_CT_DMAW >= 2);  // 2: also P == 2
   static constexpr int GD = (C + 15) / 16;
@@ -1071,23 +1079,31 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     // i - RS, whose block was read LA or more iterations earlier: RS >= LA)
     constexpr int LA = MIB_CT_LA;
     static_assert(K::RS >= LA, "ring slots cover the lookahead");
-    v4i fr[LA];
+    // FULL: the wave has NBW blocks and not the trial's last one (config B: waves 0-6), so the
+    // blocks run straight, with no wave-uniform branches between them; at every such branch the
+    // compiler drains the LDS counter (lgkmcnt(0)), which exposed each fragment read's latency
+    auto blocks = [&](auto full) {
+      constexpr bool F = decltype(full)::value;
+      v4i fr[LA];
 #pragma unroll
-    for (int j = 0; j < LA; j++)
-      if (j < n) fr[j] = frag(j);
+      for (int j = 0; j < LA; j++)
+        if (F || j < n) fr[j] = frag(j);
 #pragma unroll
-    for (int i = 0; i < K::NBW; i++) {
-      if (i < n) {  // wave-uniform
-        const int blk = l1_blk<K>(wave, i);
-        const v4i a = fr[i % LA];
-        if (i + LA < n) fr[i % LA] = frag(i + LA);
-        if (blk == K::NB1 - 1) {
-          l1_block<K, true>(a, blk, smem_y1, R, lane);
-        } else {
-          l1_block<K, false>(a, blk, smem_y1, R, lane);
+      for (int i = 0; i < K::NBW; i++) {
+        if (F || i < n) {  // wave-uniform
+          const int blk = l1_blk<K>(wave, i);
+          const v4i a = fr[i % LA];
+          if (F ? i + LA < K::NBW : i + LA < n) fr[i % LA] = frag(i + LA);
+          if (!F && blk == K::NB1 - 1) {
+            l1_block<K, true>(a, blk, smem_y1, R, lane);
+          } else {
+            l1_block<K, false>(a, blk, smem_y1, R, lane);
+          }
         }
       }
-    }
+    };
+    if (MIB_CT_FULL && n == K::NBW && l1_start<K>(wave) + K::NBW < K::NB1) blocks(BoolC<true>{});
+    else blocks(BoolC<false>{});
     prefetch_l1<K>(rnext, R, lane, wave, ring);
     return;
   }
