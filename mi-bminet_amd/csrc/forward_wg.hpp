@@ -75,6 +75,10 @@ constexpr int PRIO_L1 = MIB_PRIO_L1, PRIO_L45 = MIB_PRIO_L45;
 #ifndef MIB_W45
 #define MIB_W45 4
 #endif
+#ifndef MIB_CT_TR16
+#define MIB_CT_TR16 1  // channel-major P == 2: ds_read_b64_tr_b16 staging (Cfg::TR16)
+#endif
+
 template <bool V>
 struct BoolC {
   static constexpr bool value = V;
@@ -149,7 +153,7 @@ struct Cfg {
   // instruction measured +50 % on config C (LDS-DMA handles scattered rows far worse than VGPR loads)
   static constexpr bool DMA = CT_ && !FQ_ && (P == 2 ? MIB_CT_DMA >= 1 : MIB_CT_DMA >= 2);
   static constexpr bool GROUPS = CT_ && !FQ_ && !DMA && PF == NBW && NBW >= GB &&
-                                 (P == 2 ? (MIB_CT_PAIRS && C % 2 == 0) : (MIB_CT_QUADS && C % 16 == 0));
+                                 (P == 2 ? (MIB_CT_PAIRS && !MIB_CT_TR16 && C % 2 == 0) : (MIB_CT_QUADS && C % 16 == 0));
   static constexpr int NGRP = GROUPS ? NBW / GB : 0;
   static constexpr int NGS = NGRP * GL;                  // prefetch slots of the groups
   static_assert(!GROUPS || NGS + (NBW - NGRP * GB) == PF, "group slots + single slots = prefetched registers");
@@ -167,10 +171,15 @@ struct Cfg {
   // (samples of one parity) are contiguous and layer 2's K-window slices are 16-B aligned.
   // Otherwise (P == 1, and channel-major input, whose layer-1 MFMA rows pair samples j and j + 16,
   // so that a lane's 4 outputs are consecutive samples) the row is in natural order.
+  // Channel-major P == 2 (MIB_CT_TR16): the block image's rows are channels (32 bytes = 16 sample
+  // pairs), read with ds_read_b64_tr_b16, so MFMA row j is the sample pair (2 j, 2 j + 1) as in the
+  // time-major kernel, and the parity-split y1 rows and layer-2 fragments are the time-major ones
+  // (tr16_pos, staged_tr).  Otherwise (ds_read_b64_tr_b8) rows pair samples j and j + 16.
+  static constexpr bool TR16 = CT_ && P == 2 && MIB_CT_TR16;
 #ifdef MIB_DIAG_CT_PSPLIT
   static constexpr bool PSPLIT = P == 2;  // timing proxy (results wrong): the time-major y1 layout
 #else
-  static constexpr bool PSPLIT = P == 2 && !CT_;
+  static constexpr bool PSPLIT = P == 2 && (!CT_ || TR16);
 #endif
   static constexpr int PL = PSPLIT ? 2 : 1;             // y1 layout: planes per row
   static constexpr bool L2NAT = P == 2 && !PSPLIT;      // layer-2 bands of the natural layout (host: *_n)
@@ -467,15 +476,21 @@ __device__ __forceinline__ Rsrc trial_rsrc(const int8_t* xt, int trials_left, in
 
 // Physical row of K-slot k in a channel-major block image (see stage_block); its own inverse.
 __device__ __forceinline__ int stg_pos(int k) { return k ^ ((k >> 1) & 8); }
+// K::TR16 image: 32-byte row slot of channel c; channels c and c + 8, which the two 16-lane groups
+// of a 32-lane half read together, land in different bank halves (conflict-free, as stg_pos); its
+// own inverse.  Lane L stores / DMA-loads half L & 1 of channel tr16_pos(L >> 1) at byte 16 L.
+__device__ __forceinline__ int tr16_pos(int c) { return c ^ (((c >> 3) & 1) << 2); }
 
 template <class K>
 __device__ __forceinline__ int lane_xoff(int lane, int wave) {
   if constexpr (K::DMA) {
     // LDS-DMA ring (layer1): lane L's 16 bytes land in row L of the block image, so lane L loads
     // K-slot stg_pos(L) (P == 2: channel k >> 1, samples 16 (k & 1) .. +15 of the block; P == 1:
-    // channel k).  Lanes past the rows (C = 22: K-slots 44..63) read zeros without a fetch.
+    // channel k); K::TR16: half L & 1 of channel tr16_pos(L >> 1).  Lanes past the rows (C = 22:
+    // lanes of channels 22..31) read zeros without a fetch.
     const int k = stg_pos(lane);
-    const int c = K::P == 2 ? k >> 1 : k, h = K::P == 2 ? k & 1 : 0;
+    const int c = K::TR16 ? tr16_pos(lane >> 1) : K::P == 2 ? k >> 1 : k;
+    const int h = K::TR16 ? lane & 1 : K::P == 2 ? k & 1 : 0;
     if (c >= K::C) return (int)0x80000000u;
     return c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h;
   }
@@ -494,7 +509,7 @@ __device__ __forceinline__ int lane_xoff(int lane, int wave) {
     if (lane >= 44) return (int)0x80000000u;
     return (lane >> 2) * K::T + 16 * (lane & 3) + 32 * l1_start<K>(wave);
 #endif
-    const int c = K::P == 2 ? lane >> 1 : lane, h = K::P == 2 ? lane & 1 : 0;
+    const int c = K::TR16 ? tr16_pos(lane >> 1) : K::P == 2 ? lane >> 1 : lane, h = K::P == 2 ? lane & 1 : 0;
     if (c >= K::C) return (int)0x80000000u;
     return (K::FQ ? 4 : 1) * (c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h);
   }
@@ -596,33 +611,42 @@ __device__ __forceinline__ int stg_read_off(int lane, int r) {
   return 16 * stg_pos(16 * g + 8 * r + q) + 8 * p;
 }
 
-// IDENT: the lane already holds K-slot stg_pos(lane) (the DMA ring's lane offsets), so its row goes
-// to row lane of the image
-template <class K, bool IDENT = false>
-__device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
+// the A fragment of the block image at stg (two transposed reads).  K::TR16: lane (i, g)'s read r
+// takes channels 8 g + 4 r .. +3 as rows; lane i supplies row i >> 2, bytes 8 (i & 3) .. +7
+// (tools/tr16_probe.hip checks the map and the fragment on gfx950).
+template <class K>
+__device__ __forceinline__ v4i staged_tr(const int8_t* stg, int lane) {
   typedef int v2i __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) v2i lds_v2i;
+  if constexpr (K::TR16) {
+    typedef short v4s __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) v4s lds_v4s;
+    const int i = lane & 15, g = lane >> 4;
+    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(stg + 32 * tr16_pos(8 * g + (i >> 2)) + 8 * (i & 3)));
+    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(stg + 32 * tr16_pos(8 * g + 4 + (i >> 2)) + 8 * (i & 3)));
+    const v2i a = __builtin_bit_cast(v2i, lo), b = __builtin_bit_cast(v2i, hi);
+    return (v4i){a[0], a[1], b[0], b[1]};
+  } else {
+    const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 0)));
+    const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 1)));
+    return (v4i){lo[0], lo[1], hi[0], hi[1]};
+  }
+}
+
+// IDENT: the lane already holds K-slot stg_pos(lane) (the DMA ring's lane offsets), so its row goes
+// to row lane of the image (K::TR16: always, lane_xoff's map)
+template <class K, bool IDENT = false>
+__device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   wave_sync_lds();  // the previous block's reads precede this store
 #ifdef MIB_DIAG_CT_NOWRITE
   // timing proxy (results wrong): the transposed reads without the store (what an LDS-DMA fill,
   // which needs no VGPR -> LDS transfer, could at most save); the loaded data is kept live
   asm volatile("" ::"v"(raw));
 #else
-  *(v4i*)(stg + 16 * (IDENT ? lane : stg_pos(lane))) = raw;
+  *(v4i*)(stg + 16 * (IDENT || K::TR16 ? lane : stg_pos(lane))) = raw;
 #endif
   wave_sync_lds();
-  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 0)));
-  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 1)));
-  return (v4i){lo[0], lo[1], hi[0], hi[1]};
-}
-
-// the A fragment of the block staged at stg (two transposed reads)
-__device__ __forceinline__ v4i staged_tr(const int8_t* stg, int lane) {
-  typedef int v2i __attribute__((ext_vector_type(2)));
-  typedef __attribute__((address_space(3))) v2i lds_v2i;
-  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 0)));
-  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(stg + stg_read_off(lane, 1)));
-  return (v4i){lo[0], lo[1], hi[0], hi[1]};
+  return staged_tr<K>(stg, lane);
 }
 
 // LDS-DMA (channel-major ring, K::DMA): buffer_load_dwordx4 ... lds writes lane L's 16 bytes from
@@ -1067,7 +1091,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         asm volatile("" : "+v"(ln));
         return dw_tr<K>(ring + 1024 * K::GB * (i / K::GB), ln, i % K::GB);
       }
-      return staged_tr(ring + 1024 * i, lane);
+      return staged_tr<K>(ring + 1024 * i, lane);
     };
     auto frag = [&](int i) -> v4i {  // block i's A fragment
       if (i < K::RS) return ring_tr(i);
@@ -1176,7 +1200,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         for (int bb = 0; bb < K::GB; bb++) {
           const int i = q * K::GB + bb;
           if (i < n) {
-            const v4i a = staged_tr(stg + 1024 * bb, lane);
+            const v4i a = staged_tr<K>(stg + 1024 * bb, lane);
             const int blk = l1_blk<K>(wave, i);
             if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
             else l1_block<K, false>(a, blk, smem_y1, R, lane);
