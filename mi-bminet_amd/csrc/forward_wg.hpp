@@ -1596,6 +1596,10 @@ __device__ __forceinline__ void layer4(const int8_t* smem_y3, int8_t* smem_y4, c
       for (int j = 0; j < 16; j++) acc[j] = K::RB ? bias4(t) : ci;
       acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bw, acc, 0, 0, 0);
       const unsigned w = l4_out<K>(acc, sp, L.l4k, bias4(t));
+      // the pooling reads the accumulator on every path: sunk into the store's branch, it left the
+      // accumulator dead on the branch's execz path while the MFMA still wrote it, and a later
+      // inline-asm pack could be given those registers (tools/mfma_lint.py, write-after-write)
+      asm volatile("" ::"v"(w));
       if ((L.l4m >> t) & 1) *(unsigned short*)(smem_y4 + L.l4w + 8 * t) = (unsigned short)w;
     }
   }
