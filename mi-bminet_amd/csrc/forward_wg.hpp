@@ -1103,9 +1103,9 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     // i - RS, whose block was read LA or more iterations earlier: RS >= LA)
     constexpr int LA = MIB_CT_LA;
     static_assert(K::RS >= LA, "ring slots cover the lookahead");
-    // FULL: the wave has NBW blocks and not the trial's last one (config B: waves 0-6), so the
-    // blocks run straight, with no wave-uniform branches between them; at every such branch the
-    // compiler drains the LDS counter (lgkmcnt(0)), which exposed each fragment read's latency
+    // FULL: the wave has all NBW blocks (config B: waves 0-6), so the blocks run straight, with no
+    // wave-uniform branches between them (only the last may be the trial's last block); at every
+    // such branch the compiler drains the LDS counter (lgkmcnt(0)), exposing the reads' latency
     auto blocks = [&](auto full) {
       constexpr bool F = decltype(full)::value;
       v4i fr[LA];
@@ -1118,7 +1118,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
           const int blk = l1_blk<K>(wave, i);
           const v4i a = fr[i % LA];
           if (F ? i + LA < K::NBW : i + LA < n) fr[i % LA] = frag(i + LA);
-          if (!F && blk == K::NB1 - 1) {
+          if ((!F || i == K::NBW - 1) && blk == K::NB1 - 1) {  // a wave's blocks are contiguous
             l1_block<K, true>(a, blk, smem_y1, R, lane);
           } else {
             l1_block<K, false>(a, blk, smem_y1, R, lane);
@@ -1126,7 +1126,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         }
       }
     };
-    if (MIB_CT_FULL && n == K::NBW && l1_start<K>(wave) + K::NBW < K::NB1) blocks(BoolC<true>{});
+    if (MIB_CT_FULL && n == K::NBW) blocks(BoolC<true>{});
     else blocks(BoolC<false>{});
     prefetch_l1<K>(rnext, R, lane, wave, ring);
     return;
@@ -1230,29 +1230,36 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
       if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
       return a;
     };
+    // FULL (MIB_CT_FULL): waves with all NBW blocks run them without wave-uniform branches, as in
+    // the DMA path
+    auto blocks = [&](auto full) {
+      constexpr bool F = decltype(full)::value;
 #ifdef MIB_DIAG_CT_NOSTAGE
-    v4i an = raw(0);  // timing proxy (results wrong): the A fragment straight from the loads
+      v4i an = raw(0);  // timing proxy (results wrong): the A fragment straight from the loads
 #else
-    v4i an = stage_block<K>(raw(0), stg, lane);
+      v4i an = stage_block<K>(raw(0), stg, lane);
 #endif
 #pragma unroll
-    for (int i = 0; i < K::NBW; i++) {
-      if (i < n) {  // wave-uniform
-        const int blk = l1_blk<K>(wave, i);
-        const v4i a = an;
-        if (i + 1 < n)
+      for (int i = 0; i < K::NBW; i++) {
+        if (F || i < n) {  // wave-uniform
+          const int blk = l1_blk<K>(wave, i);
+          const v4i a = an;
+          if (F ? i + 1 < K::NBW : i + 1 < n)
 #ifdef MIB_DIAG_CT_NOSTAGE
-          an = raw(i + 1);
+            an = raw(i + 1);
 #else
-          an = stage_block<K>(raw(i + 1), stg + 1024 * ((i + 1) & 1), lane);
+            an = stage_block<K>(raw(i + 1), stg + 1024 * ((i + 1) & 1), lane);
 #endif
-        if (blk == K::NB1 - 1) {
-          l1_block<K, true>(a, blk, smem_y1, R, lane);
-        } else {
-          l1_block<K, false>(a, blk, smem_y1, R, lane);
+          if ((!F || i == K::NBW - 1) && blk == K::NB1 - 1) {  // a wave's blocks are contiguous
+            l1_block<K, true>(a, blk, smem_y1, R, lane);
+          } else {
+            l1_block<K, false>(a, blk, smem_y1, R, lane);
+          }
         }
       }
-    }
+    };
+    if (MIB_CT_FULL && n == K::NBW) blocks(BoolC<true>{});
+    else blocks(BoolC<false>{});
     prefetch_l1<K>(rnext, R);
     return;
   }
