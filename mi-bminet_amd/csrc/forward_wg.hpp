@@ -83,6 +83,10 @@ template <bool V>
 struct BoolC {
   static constexpr bool value = V;
 };
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
 
 struct L1Split {
   int cm, rm, cl;
@@ -203,7 +207,20 @@ struct Cfg {
 #endif
   static constexpr bool QL = CT_ && !FQ_ && !DMA && !GROUPS && MIB_CT_QL && C == 64 && PF == NBW && NBW >= 4;
   static constexpr int NQL = QL ? NBW / 4 : 0;          // quads (prefetch slots 4 q + j: load j of quad q)
-  static constexpr int STG = QL ? 5120 : cmax(MIB_CT_DBUF ? 2048 : 1024, 1024 * GB * (GROUPS ? 1 : 0));  // areas of 1 KB
+  // Channel-major int8, 64 channels (MIB_CT_ROWX): whole-row loads.  Wave w loads channel rows
+  // w + 8 h + 16 m (h < 2, m < 4) in 512-byte phases (2 rows x 512 bytes per load, lane-contiguous,
+  // where single-block loads read 16 bytes from each of 64 rows), and the waves exchange them
+  // through a 32 KB LDS image of one phase: [64 rows][512 bytes], read back with ds_read_b64_tr_b8
+  // (rx_*, layer1).  Phase 0 of the next trial is stored before barrier B; each further phase
+  // costs two barriers (the image consumed, the image complete).  Proxy: loads alone -15.9 % on
+  // config C (tools/ab.py --ct, MIB_DIAG_CT_ROWLOAD).
+#ifndef MIB_CT_ROWX
+#define MIB_CT_ROWX 0
+#endif
+  static constexpr bool RX = CT_ && !FQ_ && P == 1 && RB_ && C == 64 && MIB_CT_ROWX && SPL.cl == 0 &&
+                             (C * T) % 4 == 0 && !(P == 2 ? MIB_CT_DMA >= 1 : MIB_CT_DMA >= 2) && !QL && !GROUPS;
+  static constexpr int NPH = RX ? (16 * NB1 + 511) / 512 : 0;  // image phases of 512 samples
+  static constexpr int STG = RX ? 32768 / NWAVES : QL ? 5120 : cmax(MIB_CT_DBUF ? 2048 : 1024, 1024 * GB * (GROUPS ? 1 : 0));  // areas of 1 KB
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   // layer 3: tile 1 = the first L3C blocks of both filters side by side (one 16x16x64 MFMA),
   // tile 2 = the L3R outputs past 128, four per column in register 0 only (layer3)
@@ -238,7 +255,7 @@ struct Cfg {
   // DMA ring: RS slots of 1 KB per wave (one block image each).  Blocks past RS (config C: 9 blocks,
   // 6 slots) are prefetched into VGPRs (PFV) and stored into slots already consumed.
   static constexpr int RS = DMA ? cmin(NBW, (LDS_WG_MAX - OFF_STG) / (NWAVES * 1024)) : 0;
-  static constexpr int PFV = DMA ? NBW - RS : PF;       // blocks prefetched into VGPRs
+  static constexpr int PFV = DMA ? NBW - RS : RX ? 4 * NPH : PF;  // loads prefetched into VGPRs
   // DMA groups (MIB_CT_DMAW): the ring's first NGD * GB blocks are filled as groups of GB blocks
   // whose rows are read as 64-byte pieces, 4 lanes per row and 16 rows per DMA instruction (GD
   // instructions of 1 KB per group, in the group's GB slots), instead of 16 or 32 bytes of every
@@ -503,6 +520,16 @@ __device__ __forceinline__ int lane_xoff(int lane, int wave) {
     if (16 * (lane >> 4) >= K::GS) return (int)0x80000000u;
     return (lane & 15) * K::GS + 16 * (lane >> 4) + 16 * K::GS * l1_start<K>(wave);
 #endif
+#ifdef MIB_DIAG_CT_QLLOAD
+    // timing proxy (results wrong, P == 1): the load pattern of quads, 16 rows x 64 bytes per load
+    // (lane (r, k): row r + 16 (i % 4), bytes 16 k + 64 (i / 4) of the wave's range)
+    return (lane >> 2) * K::T + 16 * (lane & 3) + 16 * K::P * l1_start<K>(wave);
+#endif
+#ifdef MIB_DIAG_CT_ROWLOAD
+    // timing proxy (results wrong, P == 1): whole-row loads, 2 rows x 512 bytes per load
+    // (lane (h, k): row 2 (i % 4) + h + 8 (wave), bytes 512 (i / 4 % 2) + 16 k)
+    return ((lane >> 5) + 8 * wave) * K::T + 16 * (lane & 31);
+#endif
 #ifdef MIB_DIAG_CT_PAIR64
     // timing proxy (results wrong): the load pattern of block pairs, 11 rows x 64 bytes per load
     // (lane (c, k): channel c (+ 11 for odd slots), bytes 16 k of the pair)
@@ -533,7 +560,11 @@ __device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
   // cache policy: nt (2) for the time-major stream; none for channel-major, whose 128-byte lines
   // are read by several block loads of a wave (nt: +40 %, tools/ab.py)
   constexpr int AUX = K::CT ? MIB_CT_AUX : 2;
-#ifdef MIB_DIAG_CT_TMLOAD
+#ifdef MIB_DIAG_CT_QLLOAD
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff, 16 * (i % 4) * K::T + 64 * (i / 4), AUX);
+#elif defined(MIB_DIAG_CT_ROWLOAD)
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff, 2 * (i % 4) * K::T + 512 * ((i / 4) % 2), AUX);
+#elif defined(MIB_DIAG_CT_TMLOAD)
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * 16 * K::GS, 0, AUX);
 #elif defined(MIB_DIAG_CT_PAIR64)
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff, (i & 1) * 11 * K::T + 64 * (i >> 1), AUX);
@@ -700,6 +731,43 @@ __device__ __forceinline__ v4i dw_tr(const int8_t* grp, int lane, int b) {
   return (v4i){lo[0], lo[1], hi[0], hi[1]};
 }
 
+// Whole-row exchange (K::RX).  Load (m, ph) of wave w: lane L = (h, k) = (L >> 5, L & 31) reads bytes
+// 512 ph + 16 k of channel row c = w + 8 h + 16 m.  In the phase image, row c's 16-byte chunk k sits
+// at 512 c + 16 (k ^ rx_swz(c)): the 16 channels a 32-lane half of a transposed read takes
+// (c & 7 and bit 4 of c) then fall on 16 distinct chunk positions mod 256 bytes (conflict-free),
+// and a store's 8-lane groups still write 128 contiguous bytes.
+__device__ __forceinline__ int rx_swz(int c) { return (c & 7) | ((c >> 1) & 8); }
+template <class K>
+__device__ __forceinline__ int rx_lane_off(int lane, int wave) {
+  return (wave + 8 * (lane >> 5)) * K::T + 16 * (lane & 31);
+}
+// phase ph of the wave's rows (R.pf[4 ph + m]) into the image
+template <class K>
+__device__ __forceinline__ void rx_store(const Regs<K>& R, int ph, int8_t* img, int lane, int wave) {
+  asm volatile("" : "+v"(lane));  // addresses recomputed per store (registers across the loop spill)
+  const int h = lane >> 5, k = lane & 31;
+  wave_sync_lds();
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const int c = wave + 8 * h + 16 * m;
+    *(v4i*)(img + 512 * c + 16 * (k ^ rx_swz(c))) = R.pf[4 * ph + m];
+  }
+}
+// the A fragment of local block bl (16 samples, chunk bl) of the phase image: lane (i, g)'s read r
+// takes channels 16 g + 8 r + q (q = i >> 1), bytes 8 (i & 1) of the chunk
+__device__ __forceinline__ v4i rx_frag(const int8_t* img, int lane, int bl) {
+  typedef int v2i __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) v2i lds_v2i;
+  const int i = lane & 15, g = lane >> 4;
+  v2i v[2];
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int c = 16 * g + 8 * r + (i >> 1);
+    v[r] = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(img + 512 * c + 16 * (bl ^ rx_swz(c)) + 8 * (i & 1)));
+  }
+  return (v4i){v[0][0], v[0][1], v[1][0], v[1][1]};
+}
+
 // A block group (Cfg::GROUPS) into the GB staging areas: lane (cc, k) of load g holds channel
 // c = cc + g RPL, samples 16 k .. 16 k + 15 of the group: P == 2: block k >> 1, half k & 1, K-slot row
 // 2 c + (k & 1); P == 1: block k, K-slot row c.  Lanes past the data (P == 2) store their zeros
@@ -795,6 +863,17 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
   if constexpr (K::FQ) {  // the first block's four pieces
 #pragma unroll
     for (int m = 0; m < 4; m++) R.pf[m] = load_f<K>(r, xo, R.fq0, m);
+    return;
+  }
+  if constexpr (K::RX) {
+    int ln = lane;  // the row offset recomputed per trial (a register across the loop spills)
+    asm volatile("" : "+v"(ln));
+    const int xr = rx_lane_off<K>(ln, wave);
+#pragma unroll
+    for (int ph = 0; ph < K::NPH; ph++)
+#pragma unroll
+      for (int m = 0; m < 4; m++)
+        R.pf[4 * ph + m] = (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xr, 16 * m * K::T + 512 * ph, 0);
     return;
   }
   if constexpr (K::QL) {
@@ -1137,6 +1216,45 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
   for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
   const int n = l1_count<K>(wave);
   int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;  // channel-major staging
+  if constexpr (K::RX) {
+    // whole-row exchange: phase 0 of this trial was stored before the previous trial's barrier B
+    // (k_forward); each further phase: barrier (the image consumed), store, barrier (complete).
+    // Waves 0-6 split each phase's blocks; the last wave (layers 4-5) has none.
+    int8_t* img = smem_y1 - K::OFF_Y1 + K::OFF_STG;
+    static_assert(K::NPH >= 1 && K::NPH <= 2, "one or two image phases (T <= 1024)");
+    auto phase = [&](auto PH) {
+      constexpr int ph = decltype(PH)::value;
+      if constexpr (ph > 0) {
+        __syncthreads();
+        rx_store<K>(R, ph, img, lane, wave);
+        __syncthreads();
+      }
+      constexpr int NBP = cmin(32, K::NB1 - 32 * ph), BASE = NBP / (NWAVES - 1), REM = NBP % (NWAVES - 1);
+      constexpr int MAXP = BASE + (REM ? 1 : 0);
+      const int cnt = wave < NWAVES - 1 ? BASE + (wave < REM) : 0;
+      const int lo = wave * BASE + min(wave, REM);
+      auto frag = [&](int j) {
+        int ln = lane;  // read offsets recomputed per block (hoisted, they hold 2 MAXP registers)
+        asm volatile("" : "+v"(ln));
+        return rx_frag(img, ln, lo + j);
+      };
+      v4i an = frag(0);
+#pragma unroll
+      for (int j = 0; j < MAXP; j++) {
+        if (j < cnt) {  // wave-uniform
+          const int blk = 32 * ph + lo + j;
+          const v4i a = an;
+          if (j + 1 < cnt) an = frag(j + 1);
+          if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
+          else l1_block<K, false>(a, blk, smem_y1, R, lane);
+        }
+      }
+    };
+    phase(IntC<0>{});
+    if constexpr (K::NPH > 1) phase(IntC<1>{});
+    prefetch_l1<K>(rnext, R, lane, wave);
+    return;
+  }
   if constexpr (K::QL) {
     // quads: quad q's 4 loads are stored lane-linearly into the quad area when its first block's
     // fragment is read, MIB_CT_LA blocks ahead; the previous quad's reads were issued before (the
@@ -1673,6 +1791,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   // The first trial's fragments land before its layer 1 starts, as in k_layer (where loads still
   // in flight at layer 1 gave a rare wrong layer-1 row).  Once per workgroup.
   __builtin_amdgcn_s_waitcnt(0);
+  if constexpr (K::RX) rx_store<K>(R, 0, smem + K::OFF_STG, lane, wave);  // the first trial's phase 0
   __syncthreads();
   MIB_STAMP_INIT
   MIB_CLOCK_INIT
@@ -1736,6 +1855,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
 #if MIB_PRIO_L3 && !MIB_PRIO_L3_NORESET
     __builtin_amdgcn_s_setprio(0);
 #endif
+    // whole-row exchange: the next trial's phase 0 into the image (its previous contents were read
+    // before barrier A), so that barrier B also completes it
+    if constexpr (K::RX) rx_store<K>(R, 0, smem + K::OFF_STG, lane, wave);
     MIB_STAMP(3)
     MIB_LOOP_BARRIER();  // B
     MIB_STAMP(4)
