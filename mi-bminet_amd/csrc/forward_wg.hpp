@@ -215,7 +215,7 @@ struct Cfg {
   // costs two barriers (the image consumed, the image complete).  Proxy: loads alone -15.9 % on
   // config C (tools/ab.py --ct, MIB_DIAG_CT_ROWLOAD).
 #ifndef MIB_CT_ROWX
-#define MIB_CT_ROWX 0
+#define MIB_CT_ROWX 1
 #endif
   static constexpr bool RX = CT_ && !FQ_ && P == 1 && RB_ && C == 64 && MIB_CT_ROWX && SPL.cl == 0 &&
                              (C * T) % 4 == 0 && !(P == 2 ? MIB_CT_DMA >= 1 : MIB_CT_DMA >= 2) && !QL && !GROUPS;
