@@ -855,7 +855,13 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
     const int n = l1_count<K>(wave);  // slots past the wave's blocks stay unfilled (wave-uniform)
 #pragma unroll
     for (int i = K::NGD * K::GB; i < K::RS; i++)
+#ifdef MIB_DIAG_CT_DMACONTIG
+      // timing proxy (results wrong): every DMA reads 1 KB contiguous (chunk (wave RS + i) mod 24
+      // of the trial; the chunks past 24 repeat, mostly L2 hits)
+      if (i < n) dma_b128(r, 16 * lane, 1024 * ((wave * K::RS + i) % 24), rb + 1024 * i);
+#else
       if (i < n) dma_b128(r, xo, 16 * K::P * i, rb + 1024 * i);
+#endif
 #pragma unroll
     for (int i = 0; i < K::PFV; i++) R.pf[i] = load_a<K>(r, xo, K::RS + i);
     return;
