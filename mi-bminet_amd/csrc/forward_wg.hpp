@@ -1244,16 +1244,24 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         asm volatile("" : "+v"(ln));
         return rx_frag(img, ln, lo + j);
       };
-      v4i an = frag(0);
+      // FULL (MIB_CT_FULL): waves with MAXP blocks in this phase run them without branches
+      auto blocks = [&](auto full) {
+        constexpr bool F = decltype(full)::value;
+        v4i an = frag(0);
 #pragma unroll
-      for (int j = 0; j < MAXP; j++) {
-        if (j < cnt) {  // wave-uniform
-          const int blk = 32 * ph + lo + j;
-          const v4i a = an;
-          if (j + 1 < cnt) an = frag(j + 1);
-          if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
-          else l1_block<K, false>(a, blk, smem_y1, R, lane);
+        for (int j = 0; j < MAXP; j++) {
+          if (F || j < cnt) {  // wave-uniform
+            const int blk = 32 * ph + lo + j;
+            const v4i a = an;
+            if (F ? j + 1 < MAXP : j + 1 < cnt) an = frag(j + 1);
+            if ((!F || j == MAXP - 1) && blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
+            else l1_block<K, false>(a, blk, smem_y1, R, lane);
+          }
         }
+      };
+      if (cnt > 0) {
+        if (MIB_CT_FULL && cnt == MAXP) blocks(BoolC<true>{});
+        else blocks(BoolC<false>{});
       }
     };
     phase(IntC<0>{});
