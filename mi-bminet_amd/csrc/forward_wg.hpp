@@ -269,6 +269,9 @@ struct Cfg {
 #ifndef MIB_CT_FULL
 #define MIB_CT_FULL 1  // DMA ring: branch-free layer 1 for the waves with all NBW blocks (layer1)
 #endif
+#ifndef MIB_CT_FILL_AFTER_A
+#define MIB_CT_FILL_AFTER_A 1  // DMA ring: the next trial's fill issued after barrier A (k_forward)
+#endif
   static constexpr bool DW = DMA && (P == 1 ? MIB_CT_DMAW >= 1 : MIB_CT_DMAW >= 2);  // 2: also P == 2
   static constexpr int GD = (C + 15) / 16;
   static constexpr int NGD = DW ? RS / GB : 0;
@@ -1213,7 +1216,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     };
     if (MIB_CT_FULL && n == K::NBW) blocks(BoolC<true>{});
     else blocks(BoolC<false>{});
-    prefetch_l1<K>(rnext, R, lane, wave, ring);
+    if (!MIB_CT_FILL_AFTER_A) prefetch_l1<K>(rnext, R, lane, wave, ring);  // else k_forward, after barrier A
     return;
   }
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
@@ -1837,6 +1840,9 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     // instead of delaying layer 2's first loads (same-box A/B -1.8 %)
     const LaneTab T = ((const LaneTab*)(smem + K::OFF_LT))[ln];
     MIB_LOOP_BARRIER();  // A
+    // DMA ring (MIB_CT_FILL_AFTER_A): the next trial's fill off the layer-1 interval; the ring's
+    // reads all returned before the barrier
+    if constexpr (K::DMA && MIB_CT_FILL_AFTER_A) prefetch_l1<K>(rn, R, lane, wave, smem + K::OFF_STG + wave * K::RS * 1024);
     MIB_STAMP(1)
 #if MIB_PRIO_L23_LAST
     // the last wave is the youngest of its SIMD: at equal priority it loses the arbitration in
