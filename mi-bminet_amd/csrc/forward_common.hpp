@@ -118,10 +118,6 @@ struct DevParams {
   v4i l2t_afrag[F2 / 2][3][64];
   SmallParams sp;
   v4i l1_wfrag_ct[2][64];   // layer-1 B operand for the channel-major staging's K-slot order (stage_block)
-  // layer-2 full-tile and tail bands for the natural-order layer-1 rows (channel-major input with
-  // P == 2, Cfg::L2NAT; for P == 1 every path uses the natural order and l2_afrag / l2t_afrag)
-  v4i l2_afrag_n[F2][3][64];
-  v4i l2t_afrag_n[F2 / 2][3][64];
 };
 
 // LO: lower clip bound, -128 (the C's __CLIP_R(x, 127), clip_balanced=False) or -127
@@ -178,22 +174,15 @@ struct L1Tile {
 
 // Two requant fmas / multiplies on float bit patterns, issued as two v_fma_f32 / v_mul_f32: packed
 // f32 VALU beside MFMAs costs more issue time than the two plain instructions (same-box A/B of
-// the fused kernel: -0.5 %, 13 of 15 interleaved rounds).  MIB_PACKED_FMA restores v_pk_fma_f32.
+// the fused kernel: -0.5 %, 13 of 15 interleaved rounds).  PACKED: one v_pk_fma_f32 (layer 3, where
+// no MFMA of the wave is in flight: -0.8 %).
 template <bool PACKED = false>
 __device__ __forceinline__ f2 fma2(int a, int b, float r, float c) {
-#ifndef MIB_PACKED_FMA
   if constexpr (!PACKED)
     return (f2){__builtin_fmaf(__int_as_float(a), r, c), __builtin_fmaf(__int_as_float(b), r, c)};
-#endif
   return __builtin_elementwise_fma((f2){__int_as_float(a), __int_as_float(b)}, (f2){r, r}, (f2){c, c});
 }
-__device__ __forceinline__ f2 mul2(float a, float b, float r) {
-#ifndef MIB_PACKED_FMA
-  return (f2){a * r, b * r};
-#else
-  return (f2){a, b} * (f2){r, r};
-#endif
-}
+__device__ __forceinline__ f2 mul2(float a, float b, float r) { return (f2){a * r, b * r}; }
 
 // max(a, thr) - thr for a biased accumulator value acc = a + B and thrb = thr + B
 __device__ __forceinline__ unsigned relu_b(int acc, int thrb) {

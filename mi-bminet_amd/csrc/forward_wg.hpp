@@ -36,6 +36,9 @@
 // back as the MFMA A fragment; everything after that is the same code.
 #pragma once
 #include "forward_common.hpp"
+#ifdef MIB_DIAG
+#include "forward_diag.hpp"  // timing proxies (tools/ builds only; results wrong)
+#endif
 
 namespace mib {
 namespace wg {
@@ -45,38 +48,25 @@ constexpr int FPW = F2 / NWAVES;      // layer-2 / layer-3 filters per wave
 constexpr int NTHREADS = 64 * NWAVES;
 constexpr int WPE = 4;                // waves per SIMD (two workgroups per CU)
 constexpr int LDS_WG_MAX = 160 * 1024 / 2;  // LDS per workgroup at two workgroups per CU
-#ifndef MIB_PF_MAX
-#define MIB_PF_MAX 9
-#endif
-constexpr int PF_MAX = MIB_PF_MAX;    // layer-1 blocks per wave prefetched one trial ahead
+constexpr int PF_MAX = 9;             // layer-1 blocks per wave prefetched one trial ahead
+constexpr int PF_MAX_PLAIN = 3;       // plain BN: fewer, no spills (config B -5.4 %, C -13.6 %)
+constexpr int PF_MAX_PLAIN_CT = 2;
 static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wave");
 // Wave priorities (s_setprio): the last wave's layers 4-5 are the longest dependency chain of the
 // layer-1 interval, so that wave issues first while on them; layer 1 (HBM fragments, next-trial
 // prefetch) goes ahead of the other workgroup's layers 2-3.  Same-box A/B: -4 %.  Layer 3 (the end
-// of the barrier-B interval) at 1 as well: -1.7 %.  MIB_PRIO_TAIL / MIB_PRIO_L23_LAST are A/B knobs
-// (off: both measured slower).
-#ifndef MIB_PRIO_L1
-#define MIB_PRIO_L1 1
-#endif
-#ifndef MIB_PRIO_L3
-#define MIB_PRIO_L3 1
-#endif
-#ifndef MIB_PRIO_L45
-#define MIB_PRIO_L45 3
-#endif
-#ifndef MIB_PRIO_L23_LAST
-#define MIB_PRIO_L23_LAST 0
-#endif
-constexpr int PRIO_L1 = MIB_PRIO_L1, PRIO_L45 = MIB_PRIO_L45;
+// of the barrier-B interval) at 1 as well: -1.7 %.  About 20 other placements measured slower
+// (DESIGN.md §8).
+constexpr int PRIO_L1 = 1, PRIO_L3 = 1, PRIO_L45 = 3;
 
 // Layer-1 work split.  The last wave also runs layers 4 and 5 (in the same barrier interval as
 // the next trial's layer 1), so it takes fewer layer-1 blocks: waves 0 .. NWAVES-2 get cm blocks
 // (the first rm of them one more), the last wave cl, with layers 4-5 counted as W45 blocks.
-#ifndef MIB_W45
-#define MIB_W45 4
-#endif
-#ifndef MIB_CT_TR16
-#define MIB_CT_TR16 1  // channel-major P == 2: ds_read_b64_tr_b16 staging (Cfg::TR16)
+constexpr int W45 = 4;
+
+#ifndef MIB_DIAG
+// Timing-proxy switches (forward_diag.hpp): all off in the library.
+constexpr bool DIAG_NOL2 = false, DIAG_NOTAIL = false, DIAG_NOL3 = false, DIAG_NOL45 = false;
 #endif
 
 template <bool V>
@@ -97,7 +87,7 @@ constexpr L1Split l1_split(int nb1) {
   int bcost = 1 << 30;
   for (int cl = 0; cl <= nb1; cl++) {
     const int cm = (nb1 - cl) / nm, rm = (nb1 - cl) % nm;
-    const int hi = cmax(cm + (rm ? 1 : 0), cl + MIB_W45);
+    const int hi = cmax(cm + (rm ? 1 : 0), cl + W45);
     if (hi < bcost) {
       bcost = hi;
       best = L1Split{cm, rm, cl};
@@ -122,45 +112,15 @@ struct Cfg {
   static constexpr int NT4 = (8 * T64 + 63) / 64;       // L4 MFMAs of 64 time samples
   static constexpr L1Split SPL = l1_split(NB1);
   static constexpr int NBW = cmax(SPL.cm + (SPL.rm ? 1 : 0), SPL.cl);  // L1 blocks per wave (max)
-#ifndef MIB_PF_MAX_PLAIN
-#define MIB_PF_MAX_PLAIN 3  // plain BN: fewer prefetched blocks, no spills (config B -5.4 %, C -13.6 %)
-#endif
-#ifndef MIB_PF_MAX_PLAIN_CT
-#define MIB_PF_MAX_PLAIN_CT 2
-#endif
   // of which prefetched a trial ahead (the plain-BN builds hold more per-filter state)
   // (float input: the first block's four 16-byte pieces; the others load one block ahead)
-  static constexpr int PF = FQ_ ? 4 : cmin(NBW, RB ? PF_MAX : CT_ ? MIB_PF_MAX_PLAIN_CT : MIB_PF_MAX_PLAIN);
-#ifndef MIB_CT_PAIRS
-#define MIB_CT_PAIRS 0
-#endif
-#ifndef MIB_CT_QUADS
-#define MIB_CT_QUADS 0
-#endif
-  // Channel-major int8 with every block prefetched: block groups.  The GB blocks of a group cover
-  // 64 samples of every row and are loaded as GL loads of RPL rows x 64 bytes (lane (cc, k): row
-  // cc + g RPL, bytes 16 k), where single-block loads touch every row for 16 (P == 1) or 32 bytes;
-  // a group is staged at once into GB areas (layer1, stage_group).  P == 1 (64 channels): quads,
-  // GL = C / 16 loads of 16 rows.  P == 2: pairs, 2 loads of C / 2 rows.  Both off: same box, pairs
-  // +3.3 % on config B, quads +12.4 % on C and +8.7 % on 64x480 against the double-buffered single
-  // blocks (a group gives up the staging overlap).
-  static constexpr int GB = P == 2 ? 2 : 4;             // blocks per group
-  static constexpr int RPL = P == 2 ? C / 2 : 16;       // rows per group load
-  static constexpr int GL = P == 2 ? 2 : C / 16;        // loads per group
-  // Channel-major int8 through LDS-DMA (MIB_CT_DMA, layer1): each block's rows go from HBM straight
+  static constexpr int PF = FQ_ ? 4 : cmin(NBW, RB ? PF_MAX : CT_ ? PF_MAX_PLAIN_CT : PF_MAX_PLAIN);
+  // Channel-major int8, 22 channels, through LDS-DMA (layer1): each block's rows go from HBM straight
   // into an LDS ring with buffer_load_dwordx4 ... lds, a trial ahead, and the A fragments come back
-  // with ds_read_b64_tr_b8: no VGPR round trip, no ds_write (RS ring slots, LDS carve below).
-#ifndef MIB_CT_DMA
-#define MIB_CT_DMA 1
-#endif
-  // 1: P == 2 (22 channels) only; 2: also P == 1 (64 channels), where 64 rows of 16 bytes per DMA
-  // instruction measured +50 % on config C (LDS-DMA handles scattered rows far worse than VGPR loads)
-  static constexpr bool DMA = CT_ && !FQ_ && (P == 2 ? MIB_CT_DMA >= 1 : MIB_CT_DMA >= 2);
-  static constexpr bool GROUPS = CT_ && !FQ_ && !DMA && PF == NBW && NBW >= GB &&
-                                 (P == 2 ? (MIB_CT_PAIRS && !MIB_CT_TR16 && C % 2 == 0) : (MIB_CT_QUADS && C % 16 == 0));
-  static constexpr int NGRP = GROUPS ? NBW / GB : 0;
-  static constexpr int NGS = NGRP * GL;                  // prefetch slots of the groups
-  static_assert(!GROUPS || NGS + (NBW - NGRP * GB) == PF, "group slots + single slots = prefetched registers");
+  // with ds_read_b64_tr_b16: no VGPR round trip, no ds_write (RS ring slots, LDS carve below).  The
+  // 64-channel shapes load whole rows instead (RX): 64 rows of 16 bytes per DMA instruction measured
+  // +50 % on config C.
+  static constexpr bool DMA = CT_ && !FQ_ && P == 2;
   static constexpr int NB2 = (8 * T8 + 31) / 32;        // L2 column blocks of 32 outputs
   // full L2 tiles per filter, then a tail of TB blocks on the 16x16x64 chain when the wave's two
   // filters' tail columns fit its 16 columns (FPW * TC <= 16); otherwise (short trials, e.g.
@@ -171,56 +131,32 @@ struct Cfg {
   static constexpr int TB = TAIL ? NB2 - 32 * MT0 : 0;  // tail blocks (of 32 outputs) per filter
   static constexpr int TC = 2 * TB;                     // tail columns (of 16 outputs) per filter
   // layer-1 rows hold positions pos = t + 32 (32 leading zeros = the xcorr pad of 31, aligned).
-  // PSPLIT (time-major P == 2): parity-split planes [pos & 1][pos >> 1]: each lane's 4 outputs
-  // (samples of one parity) are contiguous and layer 2's K-window slices are 16-B aligned.
-  // Otherwise (P == 1, and channel-major input, whose layer-1 MFMA rows pair samples j and j + 16,
-  // so that a lane's 4 outputs are consecutive samples) the row is in natural order.
-  // Channel-major P == 2 (MIB_CT_TR16): the block image's rows are channels (32 bytes = 16 sample
-  // pairs), read with ds_read_b64_tr_b16, so MFMA row j is the sample pair (2 j, 2 j + 1) as in the
-  // time-major kernel, and the parity-split y1 rows and layer-2 fragments are the time-major ones
-  // (tr16_pos, staged_tr).  Otherwise (ds_read_b64_tr_b8) rows pair samples j and j + 16.
-  static constexpr bool TR16 = CT_ && P == 2 && MIB_CT_TR16;
-#ifdef MIB_DIAG_CT_PSPLIT
-  static constexpr bool PSPLIT = P == 2;  // timing proxy (results wrong): the time-major y1 layout
-#else
-  static constexpr bool PSPLIT = P == 2 && (!CT_ || TR16);
-#endif
+  // PSPLIT (P == 2): parity-split planes [pos & 1][pos >> 1]: each lane's 4 outputs (samples of one
+  // parity) are contiguous and layer 2's K-window slices are 16-B aligned.  P == 1: natural order.
+  // Channel-major P == 2 (TR16): the block image's rows are channels (32 bytes = 16 sample pairs),
+  // read with ds_read_b64_tr_b16, so MFMA row j is the sample pair (2 j, 2 j + 1) as in the
+  // time-major kernel, and the y1 rows and layer-2 fragments are the time-major ones (tr16_pos,
+  // staged_tr).  Channel-major P == 1: ds_read_b64_tr_b8 (stg_pos, rx_frag).
+  static constexpr bool TR16 = CT_ && P == 2;
+  static constexpr bool PSPLIT = P == 2;
   static constexpr int PL = PSPLIT ? 2 : 1;             // y1 layout: planes per row
-  static constexpr bool L2NAT = P == 2 && !PSPLIT;      // layer-2 bands of the natural layout (host: *_n)
   static constexpr int NPOS = cmax(cmax(32 + 16 * P * NB1, 32 * (NB2 - 1) + 96), 1024 * MT + 64);
   static constexpr int PLANE = align16((NPOS + PL - 1) / PL);
   static constexpr int Y1ROW = PL * PLANE;
   // batched trial stride (bytes): time-major trials are padded to 16 bytes, channel-major ones
   // are the caller's contiguous [B][C][T]
   static constexpr int XTRIAL = FQ ? 4 * C * T : CT ? C * T : align16(T * C);
-  // channel-major staging (layer1, CT): one layer-1 block per wave, 64 rows of 16 bytes, row =
-  // MFMA K-slot (stage_block)
-#ifndef MIB_CT_DBUF
-#define MIB_CT_DBUF 1
-#endif
-  // Channel-major int8, 64 channels, VGPR path (MIB_CT_QL): quads of 4 blocks loaded as 4 loads of
-  // 16 rows x 64 bytes (the DMA groups' lane offsets), stored lane-linearly (4 ds_write_b128 at
-  // 1 KB + 16 lane) into a 4 KB quad area and read with the groups' swizzled transposed reads
-  // (dw_tr); the blocks past the quads go through the single-block staging (1 KB area at 4 KB).
-#ifndef MIB_CT_QL
-#define MIB_CT_QL 0
-#endif
-  static constexpr bool QL = CT_ && !FQ_ && !DMA && !GROUPS && MIB_CT_QL && C == 64 && PF == NBW && NBW >= 4;
-  static constexpr int NQL = QL ? NBW / 4 : 0;          // quads (prefetch slots 4 q + j: load j of quad q)
-  // Channel-major int8, 64 channels (MIB_CT_ROWX): whole-row loads.  Wave w loads channel rows
+  // Channel-major int8, 64 channels, canonical BN (RX): whole-row loads.  Wave w loads channel rows
   // w + 8 h + 16 m (h < 2, m < 4) in 512-byte phases (2 rows x 512 bytes per load, lane-contiguous,
   // where single-block loads read 16 bytes from each of 64 rows), and the waves exchange them
   // through a 32 KB LDS image of one phase: [64 rows][512 bytes], read back with ds_read_b64_tr_b8
   // (rx_*, layer1).  Phase 0 of the next trial is stored before barrier B; each further phase
-  // costs two barriers (the image consumed, the image complete).  Proxy: loads alone -15.9 % on
-  // config C (tools/ab.py --ct, MIB_DIAG_CT_ROWLOAD).
-#ifndef MIB_CT_ROWX
-#define MIB_CT_ROWX 1
-#endif
-  static constexpr bool RX = CT_ && !FQ_ && P == 1 && RB_ && C == 64 && MIB_CT_ROWX && SPL.cl == 0 &&
-                             (C * T) % 4 == 0 && !(P == 2 ? MIB_CT_DMA >= 1 : MIB_CT_DMA >= 2) && !QL && !GROUPS;
+  // costs two barriers (the image consumed, the image complete).  Config C -19.6 %.
+  // The other 64-channel builds (plain BN, float input) stage one block at a time (stage_block),
+  // double-buffered in two 1 KB areas per wave.
+  static constexpr bool RX = CT_ && !FQ_ && P == 1 && RB_ && C == 64 && SPL.cl == 0 && (C * T) % 4 == 0;
   static constexpr int NPH = RX ? (16 * NB1 + 511) / 512 : 0;  // image phases of 512 samples
-  static constexpr int STG = RX ? 32768 / NWAVES : QL ? 5120 : cmax(MIB_CT_DBUF ? 2048 : 1024, 1024 * GB * (GROUPS ? 1 : 0));  // areas of 1 KB
+  static constexpr int STG = RX ? 32768 / NWAVES : 2048;  // staging bytes per wave
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
   // layer 3: tile 1 = the first L3C blocks of both filters side by side (one 16x16x64 MFMA),
   // tile 2 = the L3R outputs past 128, four per column in register 0 only (layer3)
@@ -252,32 +188,11 @@ struct Cfg {
   // block), so that the ring fits two workgroups per CU
   static constexpr bool L2TV = DMA && TB > 0;
   static constexpr int OFF_STG = OFF_L2T + (TB > 0 && !L2TV ? NWAVES * 3 * 64 * 16 : 0);  // CT staging / ring
-  // DMA ring: RS slots of 1 KB per wave (one block image each).  Blocks past RS (config C: 9 blocks,
-  // 6 slots) are prefetched into VGPRs (PFV) and stored into slots already consumed.
+  // DMA ring: RS slots of 1 KB per wave (one block image each), every block of the wave
   static constexpr int RS = DMA ? cmin(NBW, (LDS_WG_MAX - OFF_STG) / (NWAVES * 1024)) : 0;
-  static constexpr int PFV = DMA ? NBW - RS : RX ? 4 * NPH : PF;  // loads prefetched into VGPRs
-  // DMA groups (MIB_CT_DMAW): the ring's first NGD * GB blocks are filled as groups of GB blocks
-  // whose rows are read as 64-byte pieces, 4 lanes per row and 16 rows per DMA instruction (GD
-  // instructions of 1 KB per group, in the group's GB slots), instead of 16 or 32 bytes of every
-  // row per instruction (tools/ab.py --ct)
-#ifndef MIB_CT_DMAW
-#define MIB_CT_DMAW 0
-#endif
-#ifndef MIB_CT_LA
-#define MIB_CT_LA 1  // DMA ring: blocks of lookahead of the transposed reads (layer1)
-#endif
-#ifndef MIB_CT_FULL
-#define MIB_CT_FULL 1  // DMA ring: branch-free layer 1 for the waves with all NBW blocks (layer1)
-#endif
-#ifndef MIB_CT_FILL_AFTER_A
-#define MIB_CT_FILL_AFTER_A 1  // DMA ring: the next trial's fill issued after barrier A (k_forward)
-#endif
-  static constexpr bool DW = DMA && (P == 1 ? MIB_CT_DMAW >= 1 : MIB_CT_DMAW >= 2);  // 2: also P == 2
-  static constexpr int GD = (C + 15) / 16;
-  static constexpr int NGD = DW ? RS / GB : 0;
-  static_assert(!DW || GD <= GB, "a group's DMA instructions fit its slots");
+  static constexpr int PFV = DMA ? 0 : RX ? 4 * NPH : PF;  // loads prefetched into VGPRs
   static constexpr int LDS = OFF_STG + (DMA ? NWAVES * RS * 1024 : CT ? NWAVES * STG : 0);
-  static_assert(!DMA || RS >= 2, "the DMA ring holds at least two blocks per wave");
+  static_assert(!DMA || RS == NBW, "the DMA ring holds every layer-1 block of a wave");
   static_assert(!DMA || LDS <= LDS_WG_MAX, "two workgroups per CU");
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
   static_assert(GS % 4 == 0, "time-group stride must be dword aligned");
@@ -434,9 +349,8 @@ struct Regs {
   v4i pf[K::PFV > 0 ? K::PFV : 1];  // layer-1 fragments prefetched one trial ahead (VGPRs)
   v4i l2t[K::L2TV ? 3 : 1];  // layer-2 tail band fragments of the wave's filter pair (K::L2TV)
   int xoff;                // lane_xoff(lane)
-  int xg[(K::DW || K::QL) && K::P == 1 ? 2 : 1];  // DMA groups: lane offsets of the even / odd DMA instructions
-                                       // (dw_lane_off; P == 2: one, the swizzle ignores j)
-  int fq0;                 // float input: slot of the wave's first block in walking order (MIB_FQ_ALT)
+  int fq0;                 // float input: slot of the wave's first block in walking order (odd waves
+                           // walk backwards, layer1)
 };
 
 // ---- layer-1 input ---------------------------------------------------------------------------
@@ -503,52 +417,19 @@ __device__ __forceinline__ int tr16_pos(int c) { return c ^ (((c >> 3) & 1) << 2
 
 template <class K>
 __device__ __forceinline__ int lane_xoff(int lane, int wave) {
-  if constexpr (K::DMA) {
-    // LDS-DMA ring (layer1): lane L's 16 bytes land in row L of the block image, so lane L loads
-    // K-slot stg_pos(L) (P == 2: channel k >> 1, samples 16 (k & 1) .. +15 of the block; P == 1:
-    // channel k); K::TR16: half L & 1 of channel tr16_pos(L >> 1).  Lanes past the rows (C = 22:
-    // lanes of channels 22..31) read zeros without a fetch.
-    const int k = stg_pos(lane);
-    const int c = K::TR16 ? tr16_pos(lane >> 1) : K::P == 2 ? k >> 1 : k;
-    const int h = K::TR16 ? lane & 1 : K::P == 2 ? k & 1 : 0;
-    if (c >= K::C) return (int)0x80000000u;
-    return c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h;
-  }
   if constexpr (K::CT) {
     // channel-major: lane (c, h) (P == 2) or c (P == 1) reads 16 samples of channel row c; block
-    // slot i adds 16 P i samples.  Lanes past the rows read zeros without a fetch.
-#ifdef MIB_DIAG_CT_TMLOAD
-    // timing proxy (results wrong): every block load reads 16 P C contiguous bytes, as the
-    // time-major path does
-    if (16 * (lane >> 4) >= K::GS) return (int)0x80000000u;
-    return (lane & 15) * K::GS + 16 * (lane >> 4) + 16 * K::GS * l1_start<K>(wave);
-#endif
-#ifdef MIB_DIAG_CT_QLLOAD
-    // timing proxy (results wrong, P == 1): the load pattern of quads, 16 rows x 64 bytes per load
-    // (lane (r, k): row r + 16 (i % 4), bytes 16 k + 64 (i / 4) of the wave's range)
-    return (lane >> 2) * K::T + 16 * (lane & 3) + 16 * K::P * l1_start<K>(wave);
-#endif
-#ifdef MIB_DIAG_CT_ROWLOAD
-    // timing proxy (results wrong, P == 1): whole-row loads, 2 rows x 512 bytes per load
-    // (lane (h, k): row 2 (i % 4) + h + 8 (wave), bytes 512 (i / 4 % 2) + 16 k)
-    return ((lane >> 5) + 8 * wave) * K::T + 16 * (lane & 31);
-#endif
-#ifdef MIB_DIAG_CT_PAIR64
-    // timing proxy (results wrong): the load pattern of block pairs, 11 rows x 64 bytes per load
-    // (lane (c, k): channel c (+ 11 for odd slots), bytes 16 k of the pair)
-    if (lane >= 44) return (int)0x80000000u;
-    return (lane >> 2) * K::T + 16 * (lane & 3) + 32 * l1_start<K>(wave);
-#endif
-    const int c = K::TR16 ? tr16_pos(lane >> 1) : K::P == 2 ? lane >> 1 : lane, h = K::P == 2 ? lane & 1 : 0;
+    // slot i adds 16 P i samples.  P == 2 (TR16, and the DMA ring: lane L's 16 bytes land in row L
+    // of the block image): half L & 1 of channel tr16_pos(L >> 1).  Lanes past the rows (C = 22:
+    // lanes of channels 22..31) read zeros without a fetch.
+    const int c = K::TR16 ? tr16_pos(lane >> 1) : lane, h = K::P == 2 ? lane & 1 : 0;
     if (c >= K::C) return (int)0x80000000u;
     return (K::FQ ? 4 : 1) * (c * K::T + 16 * K::P * l1_start<K>(wave) + 16 * h);
   }
-#ifndef MIB_NO_ZERO_PAD_LANES
   // A lane whose 16-byte chunk lies wholly past the group's P * C bytes (C = 22: bytes 48..63)
   // only meets zero weights: it reads past num_records instead (offset >= 2^31 > any
   // num_records), so the hardware returns zeros without fetching and the MFMA multiplies zeros.
   if (16 * (lane >> 4) >= K::GS) return (int)0x80000000u;
-#endif
   return (lane & 15) * K::GS + 16 * (lane >> 4);
 }
 
@@ -557,40 +438,11 @@ template <class K>
 __device__ __forceinline__ v4i load_a(Rsrc r, int xoff, int i) {
   typedef unsigned v4u __attribute__((ext_vector_type(4)));
   // block stride: 16 time groups (time-major) or 16 P samples of a row (channel-major)
-#ifndef MIB_CT_AUX
-#define MIB_CT_AUX 0
-#endif
   // cache policy: nt (2) for the time-major stream; none for channel-major, whose 128-byte lines
   // are read by several block loads of a wave (nt: +40 %, tools/ab.py)
-  constexpr int AUX = K::CT ? MIB_CT_AUX : 2;
-#ifdef MIB_DIAG_CT_QLLOAD
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff, 16 * (i % 4) * K::T + 64 * (i / 4), AUX);
-#elif defined(MIB_DIAG_CT_ROWLOAD)
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff, 2 * (i % 4) * K::T + 512 * ((i / 4) % 2), AUX);
-#elif defined(MIB_DIAG_CT_TMLOAD)
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * 16 * K::GS, 0, AUX);
-#elif defined(MIB_DIAG_CT_PAIR64)
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff, (i & 1) * 11 * K::T + 64 * (i >> 1), AUX);
-#else
+  constexpr int AUX = K::CT ? 0 : 2;
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, xoff + i * (K::CT ? 16 * K::P : 16 * K::GS), 0, AUX);
-#endif
   return (v4i)v;
-}
-
-// Channel-major block groups (Cfg::GROUPS): lane (cc, k) = (L >> 2, L & 3) of load g reads bytes
-// 16 k .. 16 k + 15 of the group's 64 bytes of channel row cc + g RPL; lanes past 4 RPL read zeros.
-template <class K>
-__device__ __forceinline__ int lane_xoff_grp(int lane, int wave) {
-  if (lane >= 4 * K::RPL) return (int)0x80000000u;
-  return (lane >> 2) * K::T + 16 * (lane & 3) + 16 * K::P * l1_start<K>(wave);
-}
-template <class K>
-__device__ __forceinline__ int grp_off(int i) {  // slot i < NGS: group i / GL, load i % GL
-  return (i % K::GL) * K::RPL * K::T + 64 * (i / K::GL);
-}
-template <class K>
-__device__ __forceinline__ v4i load_grp(Rsrc r, int xoffg, int i) {
-  return (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xoffg, grp_off<K>(i), MIB_CT_AUX);
 }
 
 // The batch's last trial, channel-major: the one dword of the view that holds the trial's last
@@ -634,15 +486,11 @@ __device__ __forceinline__ void wave_sync_lds() {
 // then read different bank halves (conflict-free); stg_pos is its own inverse.
 // (stg_pos is defined above lane_xoff, whose DMA offsets use it)
 
-#ifndef MIB_TR8_QSEL
-#define MIB_TR8_QSEL 0
-#endif
 // byte offsets of lane (i, g)'s two transposed reads: lane i of a group supplies the address of
-// row q, bytes 8 p .. 8 p + 7 of its 8-row block
+// row q = i >> 1, bytes 8 p .. 8 p + 7 (p = i & 1) of its 8-row block
 __device__ __forceinline__ int stg_read_off(int lane, int r) {
   const int i = lane & 15, g = lane >> 4;
-  const int q = MIB_TR8_QSEL ? (i & 7) : (i >> 1), p = MIB_TR8_QSEL ? (i >> 3) : (i & 1);
-  return 16 * stg_pos(16 * g + 8 * r + q) + 8 * p;
+  return 16 * stg_pos(16 * g + 8 * r + (i >> 1)) + 8 * (i & 1);
 }
 
 // the A fragment of the block image at stg (two transposed reads).  K::TR16: lane (i, g)'s read r
@@ -667,18 +515,11 @@ __device__ __forceinline__ v4i staged_tr(const int8_t* stg, int lane) {
   }
 }
 
-// IDENT: the lane already holds K-slot stg_pos(lane) (the DMA ring's lane offsets), so its row goes
-// to row lane of the image (K::TR16: always, lane_xoff's map)
-template <class K, bool IDENT = false>
+// K::TR16: the lane's row goes to row lane of the image (lane_xoff's map)
+template <class K>
 __device__ __forceinline__ v4i stage_block(v4i raw, int8_t* stg, int lane) {
   wave_sync_lds();  // the previous block's reads precede this store
-#ifdef MIB_DIAG_CT_NOWRITE
-  // timing proxy (results wrong): the transposed reads without the store (what an LDS-DMA fill,
-  // which needs no VGPR -> LDS transfer, could at most save); the loaded data is kept live
-  asm volatile("" ::"v"(raw));
-#else
-  *(v4i*)(stg + 16 * (IDENT || K::TR16 ? lane : stg_pos(lane))) = raw;
-#endif
+  *(v4i*)(stg + 16 * (K::TR16 ? lane : stg_pos(lane))) = raw;
   wave_sync_lds();
   return staged_tr<K>(stg, lane);
 }
@@ -698,40 +539,6 @@ __device__ __forceinline__ unsigned lds_addr(const int8_t* p) {
 __device__ __forceinline__ void dma_b128(Rsrc r, int voff, int soff, unsigned lds) {
   asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
                :: "v"(voff), "s"(r), "s"(soff), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");  // m0: no other user in these kernels (tests/test_mfma_lint.py)
-}
-
-// DMA groups (K::DW).  Instruction j of a group fills KB j of the group's GB slots: lane L = (r, k')
-// = (L >> 2, L & 3) writes slot 4 r + k' with piece k' ^ dw_swz(c) of channel row c = 16 j + r, a
-// piece being 16 bytes of the group's 64 bytes of the row (P == 2: block k >> 1, half k & 1;
-// P == 1: block k).  The XOR swizzle makes the transposed reads conflict-free: a 32-lane half of
-// ds_read_b64_tr_b8 reads 16 channels whose 16-byte pieces then fall on 64 distinct banks.
-template <class K>
-__device__ __forceinline__ int dw_swz(int c) {
-  return K::P == 2 ? (c >> 2) & 2 : ((c >> 2) & 1) | ((c >> 3) & 2);
-}
-// lane offset of instruction j (the instruction adds 16 j T + 64 q through soffset; only j & 1
-// matters); rows past C land past the view and read zeros
-template <class K>
-__device__ __forceinline__ int dw_lane_off(int lane, int wave, int j) {
-  const int r = lane >> 2, kq = lane & 3;
-  return r * K::T + 16 * (kq ^ dw_swz<K>(16 * j + r)) + 16 * K::P * l1_start<K>(wave);
-}
-// byte offset in the group's slots of lane (i, g)'s transposed read rr of the group's block b
-template <class K>
-__device__ __forceinline__ int dw_read_off(int lane, int rr, int b) {
-  const int i = lane & 15, g = lane >> 4, q = i >> 1, p = i & 1;
-  const int kk = 16 * g + 8 * rr + q;
-  const int c = K::P == 2 ? kk >> 1 : kk, h = K::P == 2 ? kk & 1 : 0;
-  const int piece = K::P == 2 ? 2 * b + h : b;
-  return 1024 * (c >> 4) + 64 * (c & 15) + 16 * (piece ^ dw_swz<K>(c)) + 8 * p;
-}
-template <class K>
-__device__ __forceinline__ v4i dw_tr(const int8_t* grp, int lane, int b) {
-  typedef int v2i __attribute__((ext_vector_type(2)));
-  typedef __attribute__((address_space(3))) v2i lds_v2i;
-  const v2i lo = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(grp + dw_read_off<K>(lane, 0, b)));
-  const v2i hi = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_v2i*)(grp + dw_read_off<K>(lane, 1, b)));
-  return (v4i){lo[0], lo[1], hi[0], hi[1]};
 }
 
 // Whole-row exchange (K::RX).  Load (m, ph) of wave w: lane L = (h, k) = (L >> 5, L & 31) reads bytes
@@ -771,63 +578,15 @@ __device__ __forceinline__ v4i rx_frag(const int8_t* img, int lane, int bl) {
   return (v4i){v[0][0], v[0][1], v[1][0], v[1][1]};
 }
 
-// A block group (Cfg::GROUPS) into the GB staging areas: lane (cc, k) of load g holds channel
-// c = cc + g RPL, samples 16 k .. 16 k + 15 of the group: P == 2: block k >> 1, half k & 1, K-slot row
-// 2 c + (k & 1); P == 1: block k, K-slot row c.  Lanes past the data (P == 2) store their zeros
-// into rows 4 RPL .. 63 of area 0, which only meet zero weights.
-// The batch's last trial (last_trial): the dword of a load straddling the end of the input read as
-// zeros (trial_rsrc); the lane that holds it patches the 1-3 real bytes into its staged row with
-// byte loads and byte stores (once per launch, and kept out of the registers of the common path:
-// patching the registers pushed the pair build to a spill whose reload drained the prefetch).
-template <class K>
-__device__ __forceinline__ void stage_group(const v4i* r, int8_t* stg, int lane, int wave, int q, bool last_trial,
-                                            Rsrc rcur) {
-  asm volatile("" : "+v"(lane));  // store addresses recomputed per group, not hoisted out of the loop
-  const int cc = lane >> 2, k = lane & 3;
-  const bool real = lane < 4 * K::RPL;
-  const int area = 1024 * (K::P == 2 ? k >> 1 : k);
-  wave_sync_lds();  // the previous blocks' reads precede these stores
-  int w[K::GL];
-#pragma unroll
-  for (int g = 0; g < K::GL; g++) {
-    const int c = cc + g * K::RPL;
-    w[g] = real ? area + 16 * stg_pos(K::P == 2 ? 2 * c + (k & 1) : c) : 16 * lane;
-    *(v4i*)(stg + w[g]) = r[g];
-  }
-  if (last_trial) {
-    constexpr int N = K::C * K::T;
-    const int xg = lane_xoff_grp<K>(lane, wave);
-#pragma unroll
-    for (int g = 0; g < K::GL; g++) {
-      const int o = xg + grp_off<K>(q * K::GL + g);
-      if (real && o < N && N < o + 16 && ((N - o) & 3)) {
-        const int k0 = (N - o) & ~3;
-        for (int m = 0; o + k0 + m < N; m++)
-          stg[w[g] + k0 + m] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
-      }
-    }
-  }
-  wave_sync_lds();
-}
-
 // Float input, HBM traffic (float input; pmc_traffic.json b22_f32).  Float rows are
 // not 128-byte aligned, so a cache line at a border between two blocks holds bytes of both.  With
 // every wave walking forward, the next wave's first block was requested a trial ahead while this
 // wave's last block arrived at the end of layer 1, and each such line came from HBM twice (1.23x).
-// MIB_FQ_ALT: odd waves walk their blocks backwards, so both sides of every wave border are read
-// in the same phase of the trial.  MIB_FQ_PF_AT: where the next trial's first block is requested:
-// 1 at the end of layer 1, 2 after layer 2, 3 after layer 3, 4 at the start of its own layer 1 (no
-// trial-ahead request); a later request leaves less time for the line it shares with the block
-// loaded next to leave L2.  Same box: 1.231x -> 1.089x (ALT) ->
-// 1.021x (ALT + PF_AT 2), -6.9 % time (tools/ab.py --f32, profiles/r04_ab.txt).  PF_AT 4: the
-// same 1.022x and another -1.3 % (9 interleaved rounds): the other waves cover the first block's
-// latency, and the wave's registers stay free through layers 2-5.
-#ifndef MIB_FQ_ALT
-#define MIB_FQ_ALT 1
-#endif
-#ifndef MIB_FQ_PF_AT
-#define MIB_FQ_PF_AT 4
-#endif
+// So odd waves walk their blocks backwards (both sides of every wave border are read in the same
+// phase of the trial: 1.231x -> 1.089x), and a wave requests its first block at the start of its
+// own layer 1, with no trial-ahead request (1.022x, -8.1 % time in two same-box steps,
+// tools/ab.py --f32, profiles/r04_ab.txt): the other waves cover the first block's latency, and
+// the wave's registers stay free through layers 2-5.
 // float input (K::FQ): 16-byte piece m of the lane's 64 bytes of block slot i
 template <class K>
 __device__ __forceinline__ v4i load_f(Rsrc r, int xoff, int i, int m) {
@@ -842,31 +601,15 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
   int xo = R.xoff;
   asm volatile("" : "+v"(xo));
   if constexpr (K::DMA) {
-    // ring slots 0 .. RS - 1 by LDS-DMA, the rest into VGPRs.  The ring's transposed reads of the
-    // trial just computed have returned (their MFMAs consumed them); the wait makes that explicit
-    // for the hardware, which would otherwise let a DMA write race a read still queued.
+    // ring slots 0 .. RS - 1 by LDS-DMA.  The ring's transposed reads of the trial just computed
+    // have returned (their MFMAs consumed them); the wait makes that explicit for the hardware,
+    // which would otherwise let a DMA write race a read still queued.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const unsigned rb = lds_addr(ring);
-#pragma unroll
-    for (int q = 0; q < K::NGD; q++)
-#pragma unroll
-      for (int j = 0; j < K::GD; j++) {
-        int xg = R.xg[K::P == 1 ? j & 1 : 0];
-        asm volatile("" : "+v"(xg));
-        dma_b128(r, xg, 16 * j * K::T + 64 * q, rb + 1024 * (K::GB * q + j));
-      }
     const int n = l1_count<K>(wave);  // slots past the wave's blocks stay unfilled (wave-uniform)
 #pragma unroll
-    for (int i = K::NGD * K::GB; i < K::RS; i++)
-#ifdef MIB_DIAG_CT_DMACONTIG
-      // timing proxy (results wrong): every DMA reads 1 KB contiguous (chunk (wave RS + i) mod 24
-      // of the trial; the chunks past 24 repeat, mostly L2 hits)
-      if (i < n) dma_b128(r, 16 * lane, 1024 * ((wave * K::RS + i) % 24), rb + 1024 * i);
-#else
+    for (int i = 0; i < K::RS; i++)
       if (i < n) dma_b128(r, xo, 16 * K::P * i, rb + 1024 * i);
-#endif
-#pragma unroll
-    for (int i = 0; i < K::PFV; i++) R.pf[i] = load_a<K>(r, xo, K::RS + i);
     return;
   }
   if constexpr (K::FQ) {  // the first block's four pieces
@@ -885,30 +628,6 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
         R.pf[4 * ph + m] = (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xr, 16 * m * K::T + 512 * ph, 0);
     return;
   }
-  if constexpr (K::QL) {
-#pragma unroll
-    for (int q = 0; q < K::NQL; q++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        int xg = R.xg[j & 1];
-        asm volatile("" : "+v"(xg));
-        R.pf[4 * q + j] = (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xg, 16 * j * K::T + 64 * q, MIB_CT_AUX);
-      }
-#pragma unroll
-    for (int i = 4 * K::NQL; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, i);
-    return;
-  }
-  if constexpr (K::GROUPS) {
-    // the group offset is recomputed from the lane id each trial (a register across the loop spills)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int xg = lane_xoff_grp<K>(ln, wave);
-#pragma unroll
-    for (int i = 0; i < K::NGS; i++) R.pf[i] = load_grp<K>(r, xg, i);
-#pragma unroll
-    for (int i = K::NGS; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, K::NGRP * K::GB + i - K::NGS);
-    return;
-  }
 #pragma unroll
   for (int i = 0; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, i);
 }
@@ -920,10 +639,6 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   for (int t = 0; t < K::P; t++) {
     L1Tile& T = R.tile(t);
     R.xoff = lane_xoff<K>(lane, wave);
-    if constexpr (K::DW || K::QL) {
-      R.xg[0] = dw_lane_off<K>(lane, wave, 0);
-      if constexpr (K::P == 1) R.xg[K::P == 1 ? 1 : 0] = dw_lane_off<K>(lane, wave, 1);
-    }
     T.wf = K::CT ? prm->l1_wfrag_ct[t][lane] : prm->l1_wfrag[t][lane];
     T.ci = prm->l1_cinit[t][lane & 15];
     T.rr = prm->l1_r[t][lane & 15];
@@ -933,7 +648,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   for (int fi = 0; fi < FPW; fi++) {
     const int f = wave * FPW + fi;
 #pragma unroll
-    for (int s = 0; s < 3; s++) R.af[fi][s] = K::L2NAT ? prm->l2_afrag_n[f][s][lane] : prm->l2_afrag[f][s][lane];
+    for (int s = 0; s < 3; s++) R.af[fi][s] = prm->l2_afrag[f][s][lane];
     if constexpr (K::RB) {
       R.thr2[fi] = prm->l2_thrb[f];
       R.off2[fi] = prm->l2_offm[f];
@@ -944,7 +659,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
       R.r2[fi] = prm->sp.l2n_r[f];
     }
   }
-  R.fq0 = (MIB_FQ_ALT && (wave & 1)) ? l1_count<K>(wave) - 1 : 0;
+  R.fq0 = (wave & 1) ? l1_count<K>(wave) - 1 : 0;
   R.a31 = prm->l3_a1[wave][lane];
   R.a32 = prm->l3_a2[wave][lane];
   R.r3 = prm->sp.l3_r;
@@ -957,9 +672,9 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
   if (tid < 64) ((L45Tab*)(smem + K::OFF_L45))[tid] = build_l45_tab<K>(tid);
   if constexpr (K::L2TV) {
 #pragma unroll
-    for (int s = 0; s < 3; s++) R.l2t[s] = K::L2NAT ? prm->l2t_afrag_n[wave][s][lane] : prm->l2t_afrag[wave][s][lane];
+    for (int s = 0; s < 3; s++) R.l2t[s] = prm->l2t_afrag[wave][s][lane];
   } else if constexpr (K::TB > 0) {
-    const v4i* t = K::L2NAT ? &prm->l2t_afrag_n[0][0][0] : &prm->l2t_afrag[0][0][0];
+    const v4i* t = &prm->l2t_afrag[0][0][0];
     v4i* d = (v4i*)(smem + K::OFF_L2T);
     for (int i = tid; i < NWAVES * 3 * 64; i += NTHREADS) d[i] = t[i];
   }
@@ -985,17 +700,7 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
 #pragma unroll
   for (int t = 0; t < K::P; t++) {  // both N-tiles' MFMAs before either requant
     const L1Tile& T = R.tile(t);
-#ifdef MIB_DIAG_NOL1MFMA
-    accs[t] = a + T.wf;
-#elif defined(MIB_DIAG_L1K32)
-    {  // timing/energy proxy (results wrong): the same MFMA count at K = 32 (half the MAC slots)
-      typedef int v2i __attribute__((ext_vector_type(2)));
-      const long av = ((long)(unsigned)a[1] << 32) | (unsigned)a[0], bv = ((long)(unsigned)T.wf[1] << 32) | (unsigned)T.wf[0];
-      accs[t] = __builtin_amdgcn_mfma_i32_16x16x32_i8(av, bv, (v4i){T.ci, T.ci, T.ci, T.ci}, 0, 0, 0);
-    }
-#else
     accs[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, T.wf, (v4i){T.ci, T.ci, T.ci, T.ci}, 0, 0, 0);
-#endif
   }
 #pragma unroll
   for (int t = 0; t < K::P; t++) {
@@ -1008,12 +713,6 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
     const int f = (K::P == 2) ? 8 * t + (j >> 1) : j;
     const int t0 = K::PSPLIT ? 2 * (16 * blk + 4 * g) + p : K::P == 2 ? 32 * blk + 16 * p + 4 * g : 16 * blk + 4 * g;
     constexpr int SS = K::PL;  // sample stride of the lane's 4 outputs
-#ifdef MIB_DIAG_NOL1RQ
-    {
-      *(unsigned*)(smem_y1 + y1_index<K>(f, t0)) = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
-      continue;
-    }
-#endif
     // acc bits = 1.5*2^23 + (dot + off) as f32; fma(x, r, -1.5*2^23*r) == RN((dot+off)*r)
     const f2 q01 = fma2(acc[0], acc[1], T.rr, T.cc);
     const f2 q23 = fma2(acc[2], acc[3], T.rr, T.cc);
@@ -1041,30 +740,13 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
 // word (SDWA byte destination).  Checked against the two-pass quantiser on every float32 bit
 // pattern for several scales (tests/test_gpu_f32.py).
 __device__ __forceinline__ float quantize1_f(float x, float s, float y) {
-#ifdef MIB_FQ_OLD  // round-3 form (clamp to [-2s, 2s], clip after the quotient), for same-box A/B
-  x = fminf(fmaxf(x, -2.0f * s), 2.0f * s);
-  const float q0 = x * y;
-  const float r = __builtin_fmaf(-q0, s, x);
-  return __builtin_amdgcn_fmed3f(__builtin_fmaf(r, y, q0), -1.0f, 1.0f) * 127.0f;
-#else
   x = fminf(fmaxf(x, -s), s);
   const float q0 = x * y;
   const float r = __builtin_fmaf(-q0, s, x);
   return __builtin_fmaf(r, y, q0) * 127.0f;
-#endif
-}
-
-__device__ __forceinline__ int quantize1(float x, float s, float y) {
-  return (int)quantize1_f(x, s, y);  // trunc toward zero
 }
 
 __device__ __forceinline__ unsigned quantize4(v4i f, float s, float y) {
-#ifdef MIB_FQ_OLD
-  unsigned w = 0;
-#pragma unroll
-  for (int j = 0; j < 4; j++) w |= ((unsigned)quantize1(__int_as_float(f[j]), s, y) & 255u) << (8 * j);
-  return w;
-#else
   // v_cvt_i32_f32 truncates toward zero; the byte destination keeps the low 8 bits (the int8 value,
   // as |q * 127| <= 127) and leaves the word's other bytes as they are
   unsigned w;
@@ -1077,7 +759,6 @@ __device__ __forceinline__ unsigned quantize4(v4i f, float s, float y) {
   asm("v_cvt_i32_f32_sdwa %0, %1 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD"
       : "+v"(w) : "v"(quantize1_f(__int_as_float(f[3]), s, y)));
   return w;
-#endif
 }
 
 // test hook (mibminet_test_quantize_f32): the in-kernel quantiser on a flat array, four elements
@@ -1101,15 +782,15 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
                                        bool last_trial = false) {
   if constexpr (K::FQ) {
     // float32 rows: the lane's 16 samples of a block are 64 bytes (4 loads), quantised to the
-    // 16 int8 bytes the channel-major staging takes.  Block 0 was loaded during the previous
-    // trial (R.pf); block i + 1 is loaded while block i is quantised and computed.
+    // 16 int8 bytes the channel-major staging takes.  Block 0 is requested here (R.pf); block
+    // i + 1 is loaded while block i is quantised and computed.
     const int n = l1_count<K>(wave);
     int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;
-    if (MIB_FQ_PF_AT == 4) prefetch_l1<K>(rcur, R);  // no trial-ahead request: the first block now
+    prefetch_l1<K>(rcur, R);  // no trial-ahead request: the first block now
     v4i cur[4] = {R.pf[0], R.pf[1], R.pf[2], R.pf[3]};
-    // MIB_FQ_ALT: odd waves walk their blocks backwards (slot n - 1 first), so that both sides of
-    // every wave border are read in the same phase of the trial (float input)
-    const bool back = MIB_FQ_ALT && (wave & 1);
+    // odd waves walk their blocks backwards (slot n - 1 first), so that both sides of every wave
+    // border are read in the same phase of the trial (float input)
+    const bool back = wave & 1;
     // (a branch-free copy for waves with all NBW blocks, as in the channel-major int8 paths,
     // measured +2.7 % here: not kept)
 #pragma unroll
@@ -1133,39 +814,26 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         for (int m = 0; m < 4; m++) cur[m] = nxt[m];
       }
     }
-    if (MIB_FQ_PF_AT == 1) prefetch_l1<K>(rnext, R);  // else from the trial loop (k_forward)
     return;
   }
   if constexpr (K::DMA) {
     // Channel-major through the LDS-DMA ring: slots 0 .. RS - 1 hold blocks 0 .. RS - 1, filled a
-    // trial ahead (prefetch_l1); blocks past RS come from VGPRs and are stored into slots already
-    // consumed.  Block i + 1's fragment is read before block i's MFMAs and requant.
+    // trial ahead (prefetch_l1).  Block i + 1's fragment is read before block i's MFMAs and requant.
     const int n = l1_count<K>(wave);
     int8_t* ring = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::RS * 1024;
-    // this trial's fill has landed.  Issued after it: the PFV VGPR loads and, on the last wave, the
-    // previous trial's logits store, which need not complete (a vmcnt(0) here waited for that
-    // store's write acknowledgement on the critical last wave: +1,200 cycles per trial)
-    if (wave == NWAVES - 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(K::PFV + 1) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(K::PFV) : "memory");
+    // this trial's fill has landed.  Issued after it on the last wave: the previous trial's logits
+    // store, which need not complete (a vmcnt(0) there waited for that store's write
+    // acknowledgement on the critical last wave: +1,200 cycles per trial)
+    static_assert(K::PFV == 0, "no VGPR loads behind the ring fill");
+    if (wave == NWAVES - 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (last_trial) {
       // the batch's last trial: its view ends at its last byte, so the one dword straddling that
       // end landed as zeros; the lane holding it patches the 1-3 real bytes in (byte loads and
-      // stores, once per launch; blocks past RS are patched in registers by ct_tail)
+      // stores, once per launch)
       constexpr int N = K::C * K::T;
 #pragma unroll
-      for (int q = 0; q < K::NGD; q++)
-#pragma unroll
-        for (int j = 0; j < K::GD; j++) {
-          const int o = R.xg[K::P == 1 ? j & 1 : 0] + 16 * j * K::T + 64 * q;
-          if (o < N && N < o + 16 && ((N - o) & 3)) {
-            const int k0 = (N - o) & ~3;
-            for (int m = 0; o + k0 + m < N; m++)
-              ring[1024 * (K::GB * q + j) + 16 * lane + k0 + m] =
-                  (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
-          }
-        }
-#pragma unroll
-      for (int i = K::NGD * K::GB; i < K::RS; i++) {
+      for (int i = 0; i < K::RS; i++) {
         const int o = R.xoff + 16 * K::P * i;
         if (i < n && l1_blk<K>(wave, i) == K::NB1 - 1 && o < N && N < o + 16 && ((N - o) & 3)) {
           const int k0 = (N - o) & ~3;
@@ -1175,39 +843,20 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
       }
       wave_sync_lds();
     }
-    auto ring_tr = [&](int i) -> v4i {  // block i < RS
-      if (i < K::NGD * K::GB) {
-        int ln = lane;  // read offsets recomputed per block: hoisted, they hold 2 GB registers
-        asm volatile("" : "+v"(ln));
-        return dw_tr<K>(ring + 1024 * K::GB * (i / K::GB), ln, i % K::GB);
-      }
-      return staged_tr<K>(ring + 1024 * i, lane);
-    };
-    auto frag = [&](int i) -> v4i {  // block i's A fragment
-      if (i < K::RS) return ring_tr(i);
-      v4i raw = R.pf[i >= K::RS ? i - K::RS : 0];
-      if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) raw = ct_tail<K>(raw, rcur, R.xoff + 16 * K::P * i);
-      return stage_block<K, true>(raw, ring + 1024 * (i - K::RS), lane);
-    };
-    // fragments are read MIB_CT_LA blocks ahead of their MFMAs (a block past RS is stored into slot
-    // i - RS, whose block was read LA or more iterations earlier: RS >= LA)
-    constexpr int LA = MIB_CT_LA;
-    static_assert(K::RS >= LA, "ring slots cover the lookahead");
     // FULL: the wave has all NBW blocks (config B: waves 0-6), so the blocks run straight, with no
     // wave-uniform branches between them (only the last may be the trial's last block); at every
-    // such branch the compiler drains the LDS counter (lgkmcnt(0)), exposing the reads' latency
+    // such branch the compiler drains the LDS counter (lgkmcnt(0)), exposing the reads' latency.
+    // (Reading the fragments 2 or 3 blocks ahead measured slower: DESIGN.md §3.)
     auto blocks = [&](auto full) {
       constexpr bool F = decltype(full)::value;
-      v4i fr[LA];
-#pragma unroll
-      for (int j = 0; j < LA; j++)
-        if (F || j < n) fr[j] = frag(j);
+      v4i fr;
+      if (F || 0 < n) fr = staged_tr<K>(ring, lane);
 #pragma unroll
       for (int i = 0; i < K::NBW; i++) {
         if (F || i < n) {  // wave-uniform
           const int blk = l1_blk<K>(wave, i);
-          const v4i a = fr[i % LA];
-          if (F ? i + LA < K::NBW : i + LA < n) fr[i % LA] = frag(i + LA);
+          const v4i a = fr;
+          if (F ? i + 1 < K::NBW : i + 1 < n) fr = staged_tr<K>(ring + 1024 * (i + 1), lane);
           if ((!F || i == K::NBW - 1) && blk == K::NB1 - 1) {  // a wave's blocks are contiguous
             l1_block<K, true>(a, blk, smem_y1, R, lane);
           } else {
@@ -1216,10 +865,9 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         }
       }
     };
-    if (MIB_CT_FULL && n == K::NBW) blocks(BoolC<true>{});
+    if (n == K::NBW) blocks(BoolC<true>{});
     else blocks(BoolC<false>{});
-    if (!MIB_CT_FILL_AFTER_A) prefetch_l1<K>(rnext, R, lane, wave, ring);  // else k_forward, after barrier A
-    return;
+    return;  // the next trial's fill: k_forward, after barrier A
   }
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
   v4i xa[NX > 0 ? NX : 1];
@@ -1249,7 +897,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         asm volatile("" : "+v"(ln));
         return rx_frag(img, ln, lo + j);
       };
-      // FULL (MIB_CT_FULL): waves with MAXP blocks in this phase run them without branches
+      // FULL: waves with MAXP blocks in this phase run them without branches
       auto blocks = [&](auto full) {
         constexpr bool F = decltype(full)::value;
         v4i an = frag(0);
@@ -1265,7 +913,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         }
       };
       if (cnt > 0) {
-        if (MIB_CT_FULL && cnt == MAXP) blocks(BoolC<true>{});
+        if (cnt == MAXP) blocks(BoolC<true>{});
         else blocks(BoolC<false>{});
       }
     };
@@ -1276,119 +924,25 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     prefetch_l1<K>(rnext, R, lane, wave);
     return;
   }
-  if constexpr (K::QL) {
-    // quads: quad q's 4 loads are stored lane-linearly into the quad area when its first block's
-    // fragment is read, MIB_CT_LA blocks ahead; the previous quad's reads were issued before (the
-    // wave's LDS accesses execute in order)
-    auto store_quad = [&](int q) {
-      wave_sync_lds();
-#pragma unroll
-      for (int j = 0; j < 4; j++) *(v4i*)(stg + 1024 * j + 16 * lane) = R.pf[4 * q + j];
-      if (last_trial) {  // the batch's last trial: its straddling dword read as zeros (trial_rsrc)
-        constexpr int N = K::C * K::T;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const int o = R.xg[j & 1] + 16 * j * K::T + 64 * q;
-          if (o < N && N < o + 16 && ((N - o) & 3)) {
-            const int k0 = (N - o) & ~3;
-            for (int m = 0; o + k0 + m < N; m++)
-              stg[1024 * j + 16 * lane + k0 + m] = (int8_t)__builtin_amdgcn_raw_buffer_load_b8(rcur, o + k0 + m, 0, 0);
-          }
-        }
-      }
-      wave_sync_lds();
-    };
-    auto frag = [&](int i) -> v4i {
-      if (i < 4 * K::NQL) {
-        if (i % 4 == 0) store_quad(i / 4);
-        int ln = lane;  // read offsets recomputed per block (hoisted, they hold 8 registers)
-        asm volatile("" : "+v"(ln));
-        return dw_tr<K>(stg, ln, i % 4);
-      }
-      v4i raw = R.pf[i < K::PF ? i : 0];
-      if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) raw = ct_tail<K>(raw, rcur, R.xoff + 16 * K::P * i);
-      return stage_block<K>(raw, stg + 4096, lane);
-    };
-    constexpr int LA = MIB_CT_LA;
-    static_assert(LA >= 1 && LA <= 4, "a quad's reads precede the next quad's stores");
-    v4i fr[LA];
-#pragma unroll
-    for (int j = 0; j < LA; j++)
-      if (j < n) fr[j] = frag(j);
-#pragma unroll
-    for (int i = 0; i < K::NBW; i++) {
-      if (i < n) {  // wave-uniform
-        const int blk = l1_blk<K>(wave, i);
-        const v4i a = fr[i % LA];
-        if (i + LA < n) fr[i % LA] = frag(i + LA);
-        if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
-        else l1_block<K, false>(a, blk, smem_y1, R, lane);
-      }
-    }
-    prefetch_l1<K>(rnext, R, lane, wave);
-    return;
-  }
-  if constexpr (K::GROUPS) {
-    // block groups: the GB blocks of group q are staged at once (GL stores into GB areas); each
-    // block's fragment is read just before its MFMAs (registers)
-#pragma unroll
-    for (int q = 0; q < K::NGRP; q++) {
-      if (q * K::GB < n) {  // wave-uniform
-        stage_group<K>(&R.pf[q * K::GL], stg, lane, wave, q, last_trial, rcur);
-#pragma unroll
-        for (int bb = 0; bb < K::GB; bb++) {
-          const int i = q * K::GB + bb;
-          if (i < n) {
-            const v4i a = staged_tr<K>(stg + 1024 * bb, lane);
-            const int blk = l1_blk<K>(wave, i);
-            if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
-            else l1_block<K, false>(a, blk, smem_y1, R, lane);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int i = K::NGRP * K::GB; i < K::NBW; i++) {  // the blocks past the last group, one at a time
-      if (i < n) {
-        const int blk = l1_blk<K>(wave, i);
-        v4i a = R.pf[K::NGS + i - K::NGRP * K::GB];
-        if (last_trial && blk == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
-        a = stage_block<K>(a, stg, lane);
-        if (blk == K::NB1 - 1) l1_block<K, true>(a, blk, smem_y1, R, lane);
-        else l1_block<K, false>(a, blk, smem_y1, R, lane);
-      }
-    }
-    prefetch_l1<K>(rnext, R, lane, wave);
-    return;
-  }
-  if constexpr (K::CT && MIB_CT_DBUF) {
-    // block i + 1 is staged (store + transposed reads) before block i's MFMAs and requant, so the
-    // LDS round trip of the staging overlaps the previous block's work (two staging areas)
+  if constexpr (K::CT) {
+    // single-block staging (64 channels, plain BN): block i + 1 is staged (store + transposed
+    // reads) before block i's MFMAs and requant, so the LDS round trip of the staging overlaps the
+    // previous block's work (two staging areas)
     auto raw = [&](int i) -> v4i {
       v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
       if (last_trial && l1_blk<K>(wave, i) == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
       return a;
     };
-    // FULL (MIB_CT_FULL): waves with all NBW blocks run them without wave-uniform branches, as in
-    // the DMA path
+    // FULL: waves with all NBW blocks run them without wave-uniform branches, as in the DMA path
     auto blocks = [&](auto full) {
       constexpr bool F = decltype(full)::value;
-#ifdef MIB_DIAG_CT_NOSTAGE
-      v4i an = raw(0);  // timing proxy (results wrong): the A fragment straight from the loads
-#else
       v4i an = stage_block<K>(raw(0), stg, lane);
-#endif
 #pragma unroll
       for (int i = 0; i < K::NBW; i++) {
         if (F || i < n) {  // wave-uniform
           const int blk = l1_blk<K>(wave, i);
           const v4i a = an;
-          if (F ? i + 1 < K::NBW : i + 1 < n)
-#ifdef MIB_DIAG_CT_NOSTAGE
-            an = raw(i + 1);
-#else
-            an = stage_block<K>(raw(i + 1), stg + 1024 * ((i + 1) & 1), lane);
-#endif
+          if (F ? i + 1 < K::NBW : i + 1 < n) an = stage_block<K>(raw(i + 1), stg + 1024 * ((i + 1) & 1), lane);
           if ((!F || i == K::NBW - 1) && blk == K::NB1 - 1) {  // a wave's blocks are contiguous
             l1_block<K, true>(a, blk, smem_y1, R, lane);
           } else {
@@ -1397,7 +951,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
         }
       }
     };
-    if (MIB_CT_FULL && n == K::NBW) blocks(BoolC<true>{});
+    if (n == K::NBW) blocks(BoolC<true>{});
     else blocks(BoolC<false>{});
     prefetch_l1<K>(rnext, R);
     return;
@@ -1406,11 +960,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
   for (int i = 0; i < K::NBW; i++) {
     if (i < n) {  // wave-uniform
       const int blk = l1_blk<K>(wave, i);
-      v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
-      if constexpr (K::CT) {
-        if (last_trial && blk == K::NB1 - 1) a = ct_tail<K>(a, rcur, R.xoff + 16 * K::P * i);
-        a = stage_block<K>(a, stg, lane);
-      }
+      const v4i a = (i < K::PF) ? R.pf[i < K::PF ? i : 0] : xa[i >= K::PF ? i - K::PF : 0];
       if (blk == K::NB1 - 1) {  // the trial's last block: samples >= T are masked
         l1_block<K, true>(a, blk, smem_y1, R, lane);
       } else {
@@ -1529,41 +1079,12 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
       v16i acc;
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = K::RB ? pbias(fi) : R.thr2[fi];  // plain branch: C-init
-#ifdef MIB_DIAG_L2_16
-      {  // timing/energy proxy (results wrong): the full tile's 1024 outputs in the 16x16x64 shape
-         // at the same outputs per wave.  16 shifts need a 79-position window, so K = 128: 4 column
-         // tiles of 16 blocks x 2 K-steps = 8 MFMAs and 8 B reads (against 3 + 3 for 32x32x32).
-        v4i q[4];
-#pragma unroll
-        for (int ct = 0; ct < 4; ct++) {
-          v4i c4 = {pbias(fi), pbias(fi), pbias(fi), pbias(fi)};
-#pragma unroll
-          for (int ks = 0; ks < 2; ks++)
-            c4 = __builtin_amdgcn_mfma_i32_16x16x64_i8(R.af[fi][ks], *(const v4i*)(pb + 256 * ct + 64 * ks), c4, 0, 0, 0);
-          q[ct] = c4;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; i++) acc[i] = q[i >> 2][i & 3];
-      }
-      if constexpr (false)
-#endif
 #pragma unroll
       for (int s = 0; s < 3; s++)
-#ifdef MIB_DIAG_NOL2MFMA
-      {
-        const v4i bb = *(const v4i*)(pb + l2_boff<K>(s, 0));
-        acc[s] += bb[0]; acc[4 + s] += bb[1]; acc[8 + s] += bb[2]; acc[12 + s] += bb[3];
-      }
-#else
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, 0)), acc, 0, 0, 0);
-#endif
       // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
-#ifdef MIB_DIAG_NOPOOL
-      const unsigned w = acc[0] ^ acc[5] ^ acc[10] ^ acc[15];
-#else
       const unsigned w = K::RB ? l2_out<K::LO>(acc, R.thr2[fi], R.off2[fi], R.r2[fi])
                                : l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
-#endif
       int8_t* dst = smem_y2 + f * K::Y2ROW + 128 * mt + T.l2y;
       if (128 * (mt + 1) <= K::T8) {
         *(unsigned short*)dst = (unsigned short)w;
@@ -1573,57 +1094,10 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
         else if (u0 < K::T8) *dst = (int8_t)w;
       }
     }
-#ifdef MIB_DIAG_NOTAIL
-  if constexpr (false) {
-#else
-  if constexpr (K::TB > 0) {
-#endif
-#if MIB_PRIO_TAIL
-    __builtin_amdgcn_s_setprio(MIB_PRIO_TAIL);  // knob (A/B)
-#endif
+  if constexpr (K::TB > 0 && !DIAG_NOTAIL) {
     const v4i tacc = layer2_tail_mfma<K>(smem_y1, sp, T, R, wave, lane);
     layer2_tail_out<K>(tacc, smem_y2, sp, T, wave);
   }
-  // Sensitivity diagnostics (tools/ab.py builds only): extra independent work per wave and trial
-#ifdef MIB_DIAG_XVALU
-#if MIB_DIAG_XSEL == 1
-#define MIB_DIAG_XOP "v_add_u32"
-#elif MIB_DIAG_XSEL == 2
-#define MIB_DIAG_XOP "v_cvt_f32_i32"
-#else
-#define MIB_DIAG_XOP "v_max_i32"
-#endif
-  {
-    int d0 = lane, d1 = lane + 1, d2 = lane + 2, d3 = lane + 3;
-    const int xs = R.xoff;
-#pragma unroll
-    for (int i = 0; i < MIB_DIAG_XVALU / 4; i++)
-      asm volatile(MIB_DIAG_XOP " %0, %0, %4\n" MIB_DIAG_XOP " %1, %1, %4\n" MIB_DIAG_XOP " %2, %2, %4\n" MIB_DIAG_XOP " %3, %3, %4"
-                   : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3) : "v"(xs));
-    asm volatile("" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3));
-  }
-#endif
-#ifdef MIB_DIAG_XMFMA
-  {
-    v4i d = {0, 0, 0, 0};
-    const v4i bb = *(const v4i*)(smem_y1 + wave * FPW * K::Y1ROW + T.l2b);
-#pragma unroll
-    for (int i = 0; i < MIB_DIAG_XMFMA; i++) asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(d) : "v"(R.af[0][i % 3]), "v"(bb));
-    asm volatile("s_nop 7\n s_nop 7" ::"v"(d));
-  }
-#endif
-#ifdef MIB_DIAG_XLDS
-  {
-    v4i s = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < MIB_DIAG_XLDS; i++) {
-      v4i t;
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(t) : "v"(T.l2b), "i"(16 * (i % 8)));
-      s ^= t;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(s));
-  }
-#endif
 }
 
 // ---- layer 3 ---------------------------------------------------------------------------------
@@ -1647,11 +1121,7 @@ __device__ __forceinline__ void layer3(const int8_t* smem_y2, int8_t* smem_y3, c
   const v4i magic = {FMAGIC_I, FMAGIC_I, FMAGIC_I, FMAGIC_I};
   const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(R.a31, *(const v4i*)(y2w + T.l3b), magic, 0, 0, 0);
   v4i acc2 = magic, b2 = magic;
-#ifdef MIB_DIAG_NOL3T2
-  constexpr bool T2 = false;  // diagnostic (timing proxy): no tile 2
-#else
   constexpr bool T2 = K::L3RC > 0;
-#endif
   if constexpr (T2) {
     const int* p = (const int*)(y2w + T.l3b2);  // 4-byte aligned
     b2 = (v4i){p[0], p[1], p[2], p[3]};
@@ -1773,22 +1243,10 @@ __device__ __forceinline__ unsigned layer5(const int8_t* smem_y4, const SmallPar
   return z0 | (z1 << 8) | (z2 << 16) | (z3 << 24);
 }
 
-// Diagnostics only (tools/probe.hip and tools/ab.py builds; all give wrong results, for timing
-// insight): MIB_DIAG_NOBAR drops the in-loop barriers, MIB_DIAG_SAME_TRIAL makes every trial read
-// trial 0 (L2-resident), MIB_DIAG_NOL1RQ / NOPOOL / NOTAIL / NOL2 / NOL3 / NOL45 skip the
-// layer-1 requant, the layer-2 pooling, the layer-2 tail tile, layer 2, layer 3, layers 4-5;
-// MIB_DIAG_NOL1MFMA / NOL2MFMA replace the layer-1 / layer-2 full-tile MFMAs by a vector add;
-// MIB_DIAG_NOL3T2 drops layer 3's tile 2 (outputs past 128); MIB_DIAG_L1K32 runs layer 1's MFMAs
-// at K = 32.
-#ifdef MIB_DIAG_NOBAR
-#define MIB_LOOP_BARRIER() ((void)0)
-#else
+// Trial addressing.  Timing-proxy builds (tools/, -DMIB_DIAG: forward_diag.hpp) redefine these and
+// the DIAG_* switches; the library builds the forms below.
+#ifndef MIB_DIAG
 #define MIB_LOOP_BARRIER() __syncthreads()
-#endif
-#ifdef MIB_DIAG_SAME_TRIAL
-#define MIB_TRIAL_OFF(b) ((size_t)0 * (size_t)(b))
-#define MIB_TRIALS_LEFT(b) ((int)(b) < B ? 1 : 0)
-#else
 #define MIB_TRIAL_OFF(b) ((size_t)(b) * K::XTRIAL)
 #define MIB_TRIALS_LEFT(b) (B - (int)(b))
 #endif
@@ -1829,12 +1287,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     // being hoisted out of the loop (they would be live across it and spill)
     int ln = lane;
     asm volatile("" : "+v"(ln));
-#ifdef MIB_L1WAIT_STAMP
-    // diagnostic: wait for this trial's prefetched fragments here, so that stamp slot 7 holds the
-    // part of the HBM latency the previous trial did not cover
-    MIB_STAMP(6)
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#endif
     MIB_STAMP(7)
     __builtin_amdgcn_s_setprio(PRIO_L1);
     layer1<K>(rc, rn, smem + K::OFF_Y1, R, wave, lane, MIB_TRIALS_LEFT(b) == 1);
@@ -1844,42 +1296,22 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     // instead of delaying layer 2's first loads (same-box A/B -1.8 %)
     const LaneTab T = ((const LaneTab*)(smem + K::OFF_LT))[ln];
     MIB_LOOP_BARRIER();  // A
-    // DMA ring (MIB_CT_FILL_AFTER_A): the next trial's fill off the layer-1 interval; the ring's
+    // DMA ring: the next trial's fill, off the layer-1 interval (-0.8 % same box); the ring's
     // reads all returned before the barrier
-    if constexpr (K::DMA && MIB_CT_FILL_AFTER_A)
-      prefetch_l1<K>(rn, R, lane, wave, smem + K::OFF_STG + wave * K::RS * 1024);
+    if constexpr (K::DMA) prefetch_l1<K>(rn, R, lane, wave, smem + K::OFF_STG + wave * K::RS * 1024);
     MIB_STAMP(1)
-#if MIB_PRIO_L23_LAST
-    // the last wave is the youngest of its SIMD: at equal priority it loses the arbitration in
-    // layers 2-3 and reaches barrier B last, on the path to its layers 4-5
-    if (wave == NWAVES - 1) __builtin_amdgcn_s_setprio(MIB_PRIO_L23_LAST);
-#endif
-#ifndef MIB_DIAG_NOL2
-    layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, T, wave, ln);
-#endif
-    if constexpr (K::FQ && MIB_FQ_PF_AT == 2) prefetch_l1<K>(rn, R);
+    if constexpr (!DIAG_NOL2) layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, T, wave, ln);
     // layer 3 of filter f reads only y2 row f, which this wave wrote
-#ifdef MIB_DIAG_L23BAR
-    __syncthreads();
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#endif
     MIB_STAMP(2)
-#if MIB_PRIO_L3
     // layer 3 ends the barrier-B interval: at priority 1 a wave's layer 3 wins the arbitration
     // against the other waves' layer 2 (same-box A/B -1.2 ... -1.6 %; 2: -1.0 %; from the layer-2
     // tail on: -0.2 %)
-    __builtin_amdgcn_s_setprio(MIB_PRIO_L3);
-#endif
-#ifndef MIB_DIAG_NOL3
-    layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, T, wave);
-#endif
-    if constexpr (K::FQ && MIB_FQ_PF_AT == 3) prefetch_l1<K>(rn, R);
-#if MIB_PRIO_L3 && !MIB_PRIO_L3_NORESET
+    __builtin_amdgcn_s_setprio(PRIO_L3);
+    if constexpr (!DIAG_NOL3) layer3<K>(smem + K::OFF_Y2, smem + K::OFF_Y3, sp, R, T, wave);
     __builtin_amdgcn_s_setprio(0);
-#endif
     // whole-row exchange: the next trial's phase 0 into the image (its previous contents were read
     // before barrier A), so that barrier B also completes it
     if constexpr (K::RX) rx_store<K>(R, 0, smem + K::OFF_STG, lane, wave);
@@ -1888,15 +1320,15 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     MIB_STAMP(4)
     if (wave == NWAVES - 1) {
       __builtin_amdgcn_s_setprio(PRIO_L45);
-#ifdef MIB_DIAG_NOL45
-      if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = *(const unsigned*)(smem + K::OFF_Y3 + 4 * (b & 15));
-#else
-      const L45Tab L = ((const L45Tab*)(smem + K::OFF_L45))[ln];
-      layer4<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, L, ln);
-      MIB_STAMP(5)
-      const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, L);
-      if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = z;
-#endif
+      if constexpr (DIAG_NOL45) {
+        if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = *(const unsigned*)(smem + K::OFF_Y3 + 4 * (b & 15));
+      } else {
+        const L45Tab L = ((const L45Tab*)(smem + K::OFF_L45))[ln];
+        layer4<K>(smem + K::OFF_Y3, smem + K::OFF_Y4, sp, L, ln);
+        MIB_STAMP(5)
+        const unsigned z = layer5<K>(smem + K::OFF_Y4, sp, L);
+        if (ln == 0) *(unsigned*)(out + (size_t)b * N_OUT) = z;
+      }
       __builtin_amdgcn_s_setprio(0);
       MIB_STAMP(6)
     }

@@ -352,8 +352,7 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
   }
   // layer 2: A operand = banded weights; row i <-> shift n(i) so that lane (c, h) register r
   // holds output shift 16h + r (two complete pool-8 windows per lane).  PL: layer-1 row layout,
-  // 2 = parity-split planes (time-major input, C <= 32), 1 = natural order; both are built (the
-  // channel-major kernel of a C <= 32 network uses the natural one, l2_afrag_n).
+  // 2 = parity-split planes (C <= 32, either input layout), 1 = natural order (64 channels).
   auto l2_bands = [&](int PL, v4i (*afrag)[3][64]) {
     for (int f = 0; f < F2; f++)
       for (int s = 0; s < 3; s++)
@@ -392,9 +391,7 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         }
   };
   l2_bands(P, dp.l2_afrag);
-  l2_bands(1, dp.l2_afrag_n);
   l2_tail_bands(P, dp.l2t_afrag);
-  l2_tail_bands(1, dp.l2t_afrag_n);
   for (int f = 0; f < F2; f++) {
     // pooling in the biased relu form (forward_common.hpp, pool8): thr = -(off >> 3) (layer2.c)
     const int32_t thr2 = -(hp.l2_offset[f] >> 3);

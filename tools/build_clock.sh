@@ -6,6 +6,6 @@ cd "$(dirname "$0")/.."
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -Wno-unused-function -Wno-unused-result \
-    -mllvm -disable-promote-alloca-to-lds -DMIB_CLOCK $flags -o tools/clkbin_${name} tools/clock_probe.hip &
+    -mllvm -disable-promote-alloca-to-lds -DMIB_CLOCK -DMIB_DIAG $flags -o tools/clkbin_${name} tools/clock_probe.hip &
 done
 wait

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function \
-    -mllvm -disable-promote-alloca-to-lds $flags -shared -o tools/lib${name}_diag.so \
+    -mllvm -disable-promote-alloca-to-lds -DMIB_DIAG $flags -shared -o tools/lib${name}_diag.so \
     mi-bminet_amd/csrc/mibminet.hip &
 done
 wait
