@@ -9,6 +9,10 @@ each rank owns its own 65,536-trial shard: config E's static split, weak scaling
 
 For N > 1 launch under ``torch.distributed.run`` (one process per GPU); rank 0 prints ONE JSON
 line.  ``value`` = trials processed by all ranks / max-over-ranks wall time of the K timed steps.
+The ranks coordinate over a gloo (host) group only: the start barrier, the max-of-elapsed
+reduction and the per-rank record.  The data path has no collective, so no RCCL
+group is ever created, and nothing collective runs inside the K timed steps: each rank times its
+own steps (host clock around them, HIP events on its launch stream), then the ranks reduce.
 ``roofline.achieved`` = algorithmic bytes per launch (input 22*1125 B + 4 B logits per trial) /
 average kernel duration from HIP events on the launch stream.  ``cpu_baseline`` times the C
 restatement of the reference forward (oracle/, kind "port") on the host cores (rank 0, N = 1).
@@ -64,6 +68,12 @@ def parse():
                          "'pcie_inclusive', never as value")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
+
+
+# MIB_BENCH_STUB=1 (CPU tests only, tests/test_bench_cpu.py): the multi-rank bookkeeping with a
+# stand-in step on the host and no device or library compute; its lines are marked "stub" and
+# are never bench results.
+STUB = os.environ.get("MIB_BENCH_STUB") == "1"
 
 
 def _cpu_quota():
@@ -185,15 +195,17 @@ def main():
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one rank per GPU)")
     dist = None
-    # RCCL ("nccl") between the ranks; MIB_BENCH_BACKEND=gloo lets several ranks share one GPU
-    # (rehearsal of the multi-rank path on a one-GPU box)
-    backend = os.environ.get("MIB_BENCH_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if STUB:
+        dev = torch.device("cpu")
+    else:
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
     if world > 1:
+        # host-side coordination only (gloo): barriers, the max-of-elapsed reduction, the per-rank
+        # record; several ranks may also share one GPU this way (tools/gloo_rehearsal.sh)
         import torch.distributed as dist
-        dist.init_process_group(backend, init_method="env://")
+        dist.init_process_group("gloo", init_method="env://")
 
     ps = ParamSet.synthetic(seed=a.seed, C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"],
                             reorder_bn=a.variant != "plain_bn", clip_balanced=a.variant == "clip_balanced")
@@ -202,13 +214,14 @@ def main():
     B = a.batch
     g = torch.Generator(device=dev)
     g.manual_seed(a.seed * 1000 + rank)
+    sync = (lambda: None) if STUB else (lambda: torch.cuda.synchronize(dev))
     C, T = cfg["C"], cfg["T"]
     if a.layout == "f32":
         # float EEG whose quantised values spread over the int8 range (scale = 3 sigma)
         xf = torch.randn((B, C, T), dtype=torch.float32, device=dev, generator=g)
         qscale = 3.0
-        x = lib.quantize_input_torch(xf, qscale)  # the same trials as int8, time-major (CPU baseline)
-        torch.cuda.synchronize(dev)
+        x = None if STUB else lib.quantize_input_torch(xf, qscale)  # the same trials as int8, time-major (CPU baseline)
+        sync()
     elif a.layout == "ct":
         xc = torch.randint(-128, 128, (B, C, T), dtype=torch.int8, device=dev, generator=g)
         x = torch.zeros((B, stride), dtype=torch.int8, device=dev)  # the same trials, time-major
@@ -217,13 +230,15 @@ def main():
         x = torch.randint(-128, 128, (B, stride), dtype=torch.int8, device=dev, generator=g)
         x[:, C * T:] = 0
     y = torch.empty((B, 4), dtype=torch.int8, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    stream = None if STUB else torch.cuda.current_stream(dev)
+    sp = None if STUB else stream.cuda_stream
     ct_fn = lib.load().net_model_compute_batch_ct
     f32_fn = lib.load().net_model_compute_batch_f32
 
     def step():
-        if a.layout == "f32":
+        if STUB:
+            y.copy_(x[:, :4])  # stand-in work on the host
+        elif a.layout == "f32":
             rc = f32_fn(xf.data_ptr(), y.data_ptr(), B, qscale, local, sp)
             if rc:
                 raise lib.NetError(rc, "net_model_compute_batch_f32")
@@ -241,20 +256,24 @@ def main():
     while time.perf_counter() - t_settle < a.settle:
         for _ in range(20):
             step()
-        torch.cuda.synchronize(dev)
+        sync()
     for _ in range(a.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+        dist.barrier()  # gloo, host side: every rank starts its K steps together
+    sync()
     # HIP events on the launch stream bracket the K back-to-back launches (an event pair around
     # every launch leaves the GPU idle between launches: about +10 % per step on config B);
     # --per-launch-events keeps that mode for diagnostics
     nev = a.steps if a.per_launch_events else 1
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nev)]
+    ev = None if STUB else [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                            for _ in range(nev)]
     t0 = time.perf_counter()
-    if a.per_launch_events:
+    if STUB:
+        for i in range(a.steps):
+            step()
+    elif a.per_launch_events:
         for i in range(a.steps):
             ev[i][0].record(stream)
             step()
@@ -264,17 +283,18 @@ def main():
         for i in range(a.steps):
             step()
         ev[0][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kernel_ms = ([s.elapsed_time(e) for s, e in ev] if a.per_launch_events
-                 else [ev[0][0].elapsed_time(ev[0][1]) / a.steps])
+    sync()
+    elapsed = time.perf_counter() - t0  # this rank's K steps; no collective inside
+    if STUB:
+        kernel_ms = [elapsed * 1e3 / a.steps]
+    else:
+        kernel_ms = ([s.elapsed_time(e) for s, e in ev] if a.per_launch_events
+                     else [ev[0][0].elapsed_time(ev[0][1]) / a.steps])
     rank_avg_ms = float(np.mean(kernel_ms))
     per_rank = None
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        # after the timed steps: the slowest rank's wall time (gloo, host tensors)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed_max = float(t.item())
         # per-rank record (outside the timed region): which device, its kernel time and its wall time
@@ -284,7 +304,7 @@ def main():
         dist.all_gather_object(per_rank, mine)
         elapsed = elapsed_max
 
-    info = lib.launch_info(B, local, channel_major=a.layout != "tc")
+    info = {"grid": 0, "threads": 0, "lds_bytes": 0} if STUB else lib.launch_info(B, local, channel_major=a.layout != "tc")
     if rank == 0:
         # N > 1: the slowest rank's kernel average (each rank's is listed under "ranks")
         avg_kernel_s = (max(r["kernel_ms"] for r in per_rank) if per_rank else rank_avg_ms) / 1e3
@@ -329,20 +349,24 @@ def main():
                        "grid": info["grid"], "threads": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d,FQ=%d>>" % (
+                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d,FQ=%d,XR=0>>" % (
                              cfg["C"], cfg["T"], a.variant != "plain_bn", a.variant == "clip_balanced",
                              a.layout != "tc", a.layout == "f32"),
                          "avg_kernel_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes_trial * B},
             "cpu_baseline": None,
+            "requant": "exact integer division" if lib.params_exact_division() else "float (proven exact)",
         }
         if dist:
             out["ranks"] = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
-                            "devices_visible": torch.cuda.device_count(), "per_rank": per_rank,
-                            "note": "each rank times its own shard; value = all ranks' trials / max-over-ranks wall time"}
-        if a.pcie:
+                            "devices_visible": 0 if STUB else torch.cuda.device_count(), "per_rank": per_rank,
+                            "note": "each rank times its own shard; value = all ranks' trials / max-over-ranks "
+                                    "wall time; coordination over gloo (host) only, no RCCL"}
+        if STUB:
+            out["stub"] = "MIB_BENCH_STUB: host stand-in step, bookkeeping test only, not a measurement"
+        if a.pcie and not STUB:
             out["pcie_inclusive"] = pcie_inclusive(x, y, B, local, sp, stream)
-        if world == 1 and not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline and not STUB:
             out["cpu_baseline"] = cpu_baseline(ps, x, a.cpu_seconds)
         print(json.dumps(out), flush=True)
     if dist:

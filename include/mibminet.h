@@ -42,7 +42,9 @@ extern "C" {
 #define NET_ERR_NO_PARAMS (-2)   /* no parameter blob loaded */
 #define NET_ERR_UNSUPPORTED (-3) /* network dimensions without a compiled gfx950 kernel */
 #define NET_ERR_BLOB (-4)        /* malformed parameter blob */
-#define NET_ERR_RANGE (-5)       /* parameters outside the exactly-representable envelope */
+#define NET_ERR_RANGE (-5)       /* parameters on which the reference's int32 arithmetic is undefined
+                                    (overflow, zero divisor), or a float-input scale outside
+                                    [2^-60, 2^60] (net_model_compute_batch_f32) */
 #define NET_ERR_HIP (-100)       /* HIP runtime error: code = NET_ERR_HIP - hipError_t */
 
 /* ---- reference entry points (host pointers, single trial) -------------------------------- */
@@ -78,7 +80,13 @@ int net_last_error(void);
  * BN branches of layer2.c:139-210 / layer4.c:91-133.  Flag bit 1: clip every requantised output to
  * [-127, 127], the golden model's clip_balanced=True, functional.py:89-91; clear: [-128, 127] as
  * the C's __CLIP_R).  Other flag bits are rejected (NET_ERR_BLOB).  Validates, precomputes the gfx950 operand fragments and exact requantisation
- * reciprocals, and uploads lazily to each device on first use.  Replaces any previous set.  Pad
+ * constants, and uploads lazily to each device on first use.  Every set on which the reference's
+ * own int32 arithmetic is defined for every int8 input loads: sets inside the float requant
+ * envelope run the float-requant kernels, the others (e.g. large folded BN offsets) kernels that
+ * divide exactly in integers.  NET_ERR_RANGE only where the reference's arithmetic is undefined:
+ * a zero factor (or factor >> 3 in the plain branches), INT_MIN / -1, or an int32 overflow of
+ * acc + offset (layer1.c:90-91), of the pooled sum or sum + offset (layer2.c:97-111,
+ * layer4.c:99-130), or of the plain layer 4's sum of eight elements (layer4.c:113-130).  Replaces any previous set.  Pad
  * bytes of net_l1_weight_align (channels C..C_ALIGN-1) and of net_l5_weight (columns
  * T64..T64_ALIGN-1 of every row) must be zero, as gen_net_header.py writes them (NET_ERR_BLOB
  * otherwise).  Each distinct set gets its own device copy (about 72 KB per set and device), which
@@ -103,8 +111,18 @@ size_t net_trial_stride(void);
 
 /* Forward B trials resident on `device`; x: device pointer [B][trial_stride], y: device pointer
  * [B][N].  x must be 16-byte aligned and y 4-byte aligned (NET_ERR_INVALID otherwise; hipMalloc
- * and torch allocations are).  Launches on the device's null stream and waits for completion. */
+ * and torch allocations are).  Launches on the device's null stream and waits for completion.
+ * TIME-MAJOR trials ([T][C] each, the reference's own single-trial orientation): a caller holding
+ * channel-major [B][C][T] trials (SURVEY §8(b)'s layout, input.npz before gen_input_header.py:74
+ * transposes it) must call net_model_compute_batch_ct_sync / net_model_compute_batch_ct instead;
+ * the pointers carry no layout, and a [B][C][T] buffer passed here returns wrong logits. */
 int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device);
+
+/* SURVEY §8(b)'s batched signature, channel-major: x: DEVICE pointer to B trials [B][C][T] int8,
+ * contiguous (trial stride C*T bytes, any alignment); y: DEVICE pointer [B][N], 4-byte aligned.
+ * Launches on the device's null stream and waits for completion (net_model_compute_batch_ct is
+ * the stream-ordered form). */
+int net_model_compute_batch_ct_sync(const int8_t* x, int8_t* y, size_t B, int device);
 
 /* Same, enqueued on `stream` (a hipStream_t of `device`, NULL = null stream), no host sync. */
 int net_model_compute_batch_async(const int8_t* x, int8_t* y, size_t B, int device, void* stream);

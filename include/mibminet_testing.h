@@ -3,8 +3,9 @@
  *
  * The library turns every C truncating division of the path, y = clip(trunc(v / fac)), into a
  * float multiply by a reciprocal r that it chooses and verifies on the host (DESIGN.md §3,
- * "Exact requantisation").  This hook exposes that choice so the tests can check it against
- * exhaustive integer division on the CPU.
+ * "Exact requantisation"), or, for parameter sets outside that envelope, into an exact integer
+ * division by a magic multiplier.  These hooks expose both so the tests can check them against
+ * exhaustive integer division.
  */
 #ifndef MIBMINET_TESTING_H
 #define MIBMINET_TESTING_H
@@ -44,6 +45,19 @@ int mibminet_test_upload_stats(int64_t* uploads, int64_t* uploads_while_enqueuei
 
 /* Number of parameter-image copies resident on `device`. */
 int mibminet_test_device_images(int device);
+
+/* Exact-division builds (Cfg::XR, parameter sets outside the float requant envelope): the
+ * integer division the kernels use at layers 1, 2 and 4 (forward_common.hpp, xdiv; constants from
+ * mibminet.hip, xdiv_consts).  _host: the device instruction sequence emulated on the host,
+ * q[i] = xdiv(e[i], d) for i < n (no device needed).  _gpu: the device function itself over
+ * e = e0 .. e0 + count - 1 against C division in 64 bits, on `device`; *mismatches = the number of
+ * e where they differ.  d != 0 (NET_ERR_INVALID otherwise). */
+int mibminet_test_xdiv_host(const int32_t* e, size_t n, int32_t d, int32_t* q);
+int mibminet_test_xdiv_gpu(int32_t d, int64_t e0, int64_t count, int64_t* mismatches, int device);
+
+/* 1 when the loaded parameter set runs the exact-division kernels, 0 when the float requant
+ * kernels, NET_ERR_NO_PARAMS when none is loaded. */
+int mibminet_test_params_xr(void);
 
 #ifdef __cplusplus
 }

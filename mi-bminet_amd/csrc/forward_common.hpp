@@ -4,7 +4,8 @@
 // Requantisation y = clip(trunc((acc + off) / fac), -128, 127) is computed as
 // clip(int(float(acc + off) * r)) with r chosen on the host (mibminet.hip: choose_reciprocal) and
 // verified at every step boundary of the clipped output range, so it is bit-exact to C's integer
-// division for every reachable accumulator.
+// division for every reachable accumulator.  Parameter sets outside that float envelope run the
+// exact-division builds (Cfg::XR: xdiv below) at layers 1, 2 and 4.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -77,19 +78,37 @@ __host__ __device__ constexpr int odd_dwords(int x) { return ((x + 3) / 4 % 2) ?
 struct SmallParams {
   v4i l4_bfrag[64];       // layer-4 B operand per lane (block diagonal, see host)
   v4i l2_tpar[F2];        // layer-2 tail per filter: {PBIAS_TAIL + thr, off + 8 thr, bits of r, 0}
-                          // (thr = -(net_l2_offset >> 3); off + 8 thr = net_l2_offset & 7)
-  int l4_thr[F2];         // -(net_l4_offset >> 3)
+                          // (thr = -(net_l2_offset >> 3); off + 8 thr = net_l2_offset & 7);
+                          // XR: {.., .., xdiv magic, shift word}
+  int l4_thr[F2];         // -(net_l4_offset >> 3), clamped to the conv range (mibminet.hip)
   int l4_offm[F2];        // net_l4_offset + 8 thr
-  float l4_r[F2];
+  union {
+    float l4_r[F2];
+    unsigned l4_m[F2];    // XR: xdiv magic
+  };
   // plain (non-REORDER_BN) layer-2/4 branches: per-element BN with offset >> 3 and factor >> 3 in
   // the floor form (mibminet.hip, choose_floor_form): MFMA C-init = per-filter magic bits + offset,
-  // reciprocal r and integer-valued c, so that fma(acc bits, r, c) = FMAGIC + floor(element)
+  // reciprocal r and integer-valued c, so that fma(acc bits, r, c) = FMAGIC + floor(element).
+  // XR: C-init = offset >> 3, xdiv magic and shift word; l2_xs / l4_xs are also the shift words of
+  // the REORDER_BN builds' layer-2 / layer-4 requant (whose plain fields are unused)
   int l2n_ci[F2];
-  float l2n_r[F2];
-  float l2n_c[F2];
+  union {
+    float l2n_r[F2];
+    unsigned l2n_m[F2];
+  };
+  union {
+    float l2n_c[F2];
+    int l2_xs[F2];
+  };
   int l4n_ci[F2];
-  float l4n_r[F2];
-  float l4n_c[F2];
+  union {
+    float l4n_r[F2];
+    unsigned l4n_m[F2];
+  };
+  union {
+    float l4n_c[F2];
+    int l4_xs[F2];
+  };
   int l5_w[N_OUT][ND5_MAX];  // [k][v] with row stride T64_ALIGN, zero padded
   int l5_b[N_OUT];
   float l3_r;
@@ -101,13 +120,22 @@ struct SmallParams {
 // Operand fragments and requantisation constants, built by the host from the net.h arrays.
 struct DevParams {
   v4i l1_wfrag[2][64];      // layer-1 B operand per N-tile and lane
-  int l1_cinit[2][16];      // offset + FMAGIC_I per N-tile column
-  float l1_r[2][16];        // reciprocal per N-tile column
-  float l1_c[2][16];        // -(1.5 * 2^23) * r, exact
+  int l1_cinit[2][16];      // offset + FMAGIC_I per N-tile column (XR: offset)
+  union {
+    float l1_r[2][16];      // reciprocal per N-tile column
+    unsigned l1_m[2][16];   // XR: xdiv magic
+  };
+  union {
+    float l1_c[2][16];      // -(1.5 * 2^23) * r, exact
+    int l1_xs[2][16];       // XR: xdiv shift word
+  };
   v4i l2_afrag[F2][3][64];  // layer-2 A operand (banded weights) per filter, K-step and lane
-  int l2_thrb[F2];          // pbias(f & 1) + thr, thr = -(net_l2_offset >> 3): full-tile threshold
+  int l2_thrb[F2];          // pbias(f & 1) + thr, thr = -(net_l2_offset >> 3) clamped: full-tile threshold
   int l2_offm[F2];          // net_l2_offset + 8 thr
-  float l2_r[F2];
+  union {
+    float l2_r[F2];
+    unsigned l2_m[F2];      // XR: xdiv magic (shift word: sp.l2_xs)
+  };
   // layer-3 A operands per filter pair (wave) and lane, MFMA 16x16x64 with a block-diagonal K
   // (forward_wg.hpp, layer3): tile 1 = 16 shifts x both filters' 32-slot bands, tile 2 = the same
   // with shift g on row 4g and the other rows zero
@@ -183,6 +211,20 @@ __device__ __forceinline__ f2 fma2(int a, int b, float r, float c) {
   return __builtin_elementwise_fma((f2){__int_as_float(a), __int_as_float(b)}, (f2){r, r}, (f2){c, c});
 }
 __device__ __forceinline__ f2 mul2(float a, float b, float r) { return (f2){a * r, b * r}; }
+
+// Exact C division trunc(e / d) for every int32 e and d != 0 (the reference's int32 division;
+// INT_MIN / -1 is refused at load), for the exact-division builds (Cfg::XR).  m and xs come from
+// the host (mibminet.hip, xdiv_consts: m = ceil(2^(31 + l) / |d|), l = ceil(log2 |d|), xs = l |
+// sign(d) << 31): floor(|e| / |d|) is bits 31 .. 62 of the 64-bit product |e| m shifted right by
+// l (v_mad_u64_u32, v_alignbit_b32, v_lshrrev_b32; the shift uses bits 0-4 of xs), then the sign
+// of e / d is restored.  Proof and host emulation: mibminet.hip; tests/test_xdiv.py.
+__device__ __forceinline__ int xdiv(int e, unsigned m, int xs) {
+  const int es = e >> 31;
+  const unsigned x = (unsigned)((e ^ es) - es);  // |e|, 2^31 for INT_MIN
+  const unsigned q = (unsigned)(((unsigned long long)x * m) >> 31) >> (xs & 31);
+  const int sg = (e ^ xs) >> 31;                  // the quotient is negative
+  return (int)((q ^ (unsigned)sg) - (unsigned)sg);
+}
 
 // max(a, thr) - thr for a biased accumulator value acc = a + B and thrb = thr + B
 __device__ __forceinline__ unsigned relu_b(int acc, int thrb) {

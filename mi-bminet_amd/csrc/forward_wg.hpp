@@ -96,9 +96,10 @@ constexpr L1Split l1_split(int nb1) {
   return best;
 }
 
-template <int C_, int T_, bool RB_ = true, bool CB_ = false, bool CT_ = false, bool FQ_ = false>
+template <int C_, int T_, bool RB_ = true, bool CB_ = false, bool CT_ = false, bool FQ_ = false, bool XR_ = false>
 struct Cfg {
   static constexpr int C = C_, T = T_;
+  static constexpr bool XR = XR_;                       // exact integer division at layers 1, 2, 4 (xdiv)
   static constexpr bool FQ = FQ_;                       // float32 channel-major trials, quantised in layer1
   static_assert(!FQ_ || CT_, "float input is channel-major");
   static constexpr bool RB = RB_;                       // -DREORDER_BN variant (canonical)
@@ -342,7 +343,8 @@ struct Regs {
   __device__ __forceinline__ L1Tile& tile(int t) { return t == 0 ? t0 : t1; }
   v4i af[FPW][3];          // layer-2 band fragments of the wave's filters
   int thr2[FPW], off2[FPW];  // REORDER_BN: biased threshold, offset + 8 thr; plain: MFMA C-init, magic c bits
-  float r2[FPW];
+  float r2[FPW];             // reciprocal (XR: bits of the xdiv magic)
+  int xs2[FPW];              // XR: xdiv shift word
   v4i a31, a32;            // layer-3 tile-1 / tile-2 band fragments of the wave's filter pair
   float r3, c3;            // layer-3 requant constants (uniform)
   float qs, qy;            // float input's quantisation scale and RN(1 / scale) (K::FQ)
@@ -658,6 +660,7 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
       R.off2[fi] = __float_as_int(prm->sp.l2n_c[f]);
       R.r2[fi] = prm->sp.l2n_r[f];
     }
+    if constexpr (K::XR) R.xs2[fi] = prm->sp.l2_xs[f];
   }
   R.fq0 = (wave & 1) ? l1_count<K>(wave) - 1 : 0;
   R.a31 = prm->l3_a1[wave][lane];
@@ -713,10 +716,16 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
     const int f = (K::P == 2) ? 8 * t + (j >> 1) : j;
     const int t0 = K::PSPLIT ? 2 * (16 * blk + 4 * g) + p : K::P == 2 ? 32 * blk + 16 * p + 4 * g : 16 * blk + 4 * g;
     constexpr int SS = K::PL;  // sample stride of the lane's 4 outputs
-    // acc bits = 1.5*2^23 + (dot + off) as f32; fma(x, r, -1.5*2^23*r) == RN((dot+off)*r)
-    const f2 q01 = fma2(acc[0], acc[1], T.rr, T.cc);
-    const f2 q23 = fma2(acc[2], acc[3], T.rr, T.cc);
-    int y[4] = {(int)q01[0], (int)q01[1], (int)q23[0], (int)q23[1]};  // trunc toward zero
+    int y[4];
+    if constexpr (K::XR) {  // acc = dot + off (C-init = off): exact division
+#pragma unroll
+      for (int r = 0; r < 4; r++) y[r] = xdiv(acc[r], __float_as_uint(T.rr), __float_as_int(T.cc));
+    } else {
+      // acc bits = 1.5*2^23 + (dot + off) as f32; fma(x, r, -1.5*2^23*r) == RN((dot+off)*r)
+      const f2 q01 = fma2(acc[0], acc[1], T.rr, T.cc);
+      const f2 q23 = fma2(acc[2], acc[3], T.rr, T.cc);
+      y[0] = (int)q01[0]; y[1] = (int)q01[1]; y[2] = (int)q23[0]; y[3] = (int)q23[1];  // trunc toward zero
+    }
     if constexpr (MAYBE_LAST) {
 #pragma unroll
       for (int r = 0; r < 4; r++) y[r] = (t0 + SS * r < K::T) ? y[r] : 0;
@@ -1004,9 +1013,27 @@ __device__ __forceinline__ unsigned l2n_out(const v16i& acc, float r, float c) {
   return (s0 >> 3) | ((s1 >> 3) << 8);
 }
 
+// XR: one plain-branch element, exactly: clamp(trunc(x / fac), 0, EMAX) (acc = x with C-init = the
+// offset; the ReLU makes the lower clip bound 0)
+template <int EMAX>
+__device__ __forceinline__ int xelem(int x, unsigned m, int xs) {
+  return min(max(xdiv(x, m, xs), 0), EMAX);
+}
+template <int BASE, int EMAX>
+__device__ __forceinline__ int xelem_sum8(const v16i& acc, unsigned m, int xs) {
+  int e[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) e[i] = xelem<EMAX>(acc[BASE + i], m, xs);
+  return ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+}
+
 // Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].
-template <int LO>
-__device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, float r) {
+template <int LO, bool XR>
+__device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, float r, int xs) {
+  if constexpr (XR) {
+    const unsigned m = __float_as_uint(r);
+    return sat8x2<LO>(xdiv(pool8b<0>(acc, thr, off), m, xs), xdiv(pool8b<8>(acc, thr, off), m, xs));
+  }
   const f2 q = mul2((float)pool8b<0>(acc, thr, off), (float)pool8b<8>(acc, thr, off), r);
   return sat8x2<LO>((int)q[0], (int)q[1]);
 }
@@ -1050,6 +1077,10 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
   if constexpr (K::RB) {
     const int thrb = tp[0];
     part = (int)((relu_b(tacc[0], thrb) + relu_b(tacc[1], thrb)) + (relu_b(tacc[2], thrb) + relu_b(tacc[3], thrb)));
+  } else if constexpr (K::XR) {  // exact elements (xelem)
+    const unsigned m = sp->l2n_m[fcol];
+    const int xs = sp->l2_xs[fcol];
+    part = (xelem<127>(tacc[0], m, xs) + xelem<127>(tacc[1], m, xs)) + (xelem<127>(tacc[2], m, xs) + xelem<127>(tacc[3], m, xs));
   } else {
     const float r = sp->l2n_r[fcol], c = sp->l2n_c[fcol];  // floor form (l2n_out)
     const f2 q01 = floor_form2<127>(tacc[0], tacc[1], r, c), q23 = floor_form2<127>(tacc[2], tacc[3], r, c);
@@ -1059,7 +1090,8 @@ __device__ __forceinline__ void layer2_tail_out(const v4i tacc, int8_t* smem_y2,
   const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)part, (unsigned)part, false, false);
   const int tot = (int)sw[0] + (int)sw[1];  // whole window (rows 2k and 2k+1 hold the same)
   int y;
-  if constexpr (K::RB) y = rq<K::LO>(tot + tp[1], __int_as_float(tp[2]));
+  if constexpr (K::RB && K::XR) y = min(max(xdiv(tot + tp[1], (unsigned)tp[2], tp[3]), K::LO), 127);
+  else if constexpr (K::RB) y = rq<K::LO>(tot + tp[1], __int_as_float(tp[2]));
   else y = tot >> 3;
   if (T.ty >= 0) smem_y2[wave * FPW * K::Y2ROW + T.ty] = (int8_t)y;
 }
@@ -1083,8 +1115,15 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
       for (int s = 0; s < 3; s++)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, 0)), acc, 0, 0, 0);
       // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
-      const unsigned w = K::RB ? l2_out<K::LO>(acc, R.thr2[fi], R.off2[fi], R.r2[fi])
-                               : l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
+      unsigned w;
+      if constexpr (K::RB) {
+        w = l2_out<K::LO, K::XR>(acc, R.thr2[fi], R.off2[fi], R.r2[fi], K::XR ? R.xs2[fi] : 0);
+      } else if constexpr (K::XR) {
+        const unsigned m = __float_as_uint(R.r2[fi]);
+        w = (unsigned)(xelem_sum8<0, 127>(acc, m, R.xs2[fi]) >> 3) | ((unsigned)(xelem_sum8<8, 127>(acc, m, R.xs2[fi]) >> 3) << 8);
+      } else {
+        w = l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
+      }
       int8_t* dst = smem_y2 + f * K::Y2ROW + 128 * mt + T.l2y;
       if (128 * (mt + 1) <= K::T8) {
         *(unsigned short*)dst = (unsigned short)w;
@@ -1163,8 +1202,12 @@ __device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* s
   if constexpr (K::RB) {
     const int thrb = MIB_K4(sp->l4_thr, int) + bias, offm = MIB_K4(sp->l4_offm, int);
     const float r4 = MIB_K4(sp->l4_r, float);
-    const f2 q = mul2((float)pool8b<0>(acc, thrb, offm), (float)pool8b<8>(acc, thrb, offm), r4);
-    return sat8x2<K::LO>((int)q[0], (int)q[1]);
+    return l2_out<K::LO, K::XR>(acc, thrb, offm, r4, K::XR ? MIB_K4(sp->l4_xs, int) : 0);
+  } else if constexpr (K::XR) {
+    const unsigned m = MIB_K4(sp->l4n_m, unsigned);
+    const int xs = MIB_K4(sp->l4_xs, int);
+    const int sm[2] = {min(xelem_sum8<0, 1024>(acc, m, xs) >> 3, 127), min(xelem_sum8<8, 1024>(acc, m, xs) >> 3, 127)};
+    return (unsigned)sm[0] | ((unsigned)sm[1] << 8);
   } else {
     // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
     // sum of 8, >> 3, clip.  Elements in the floor form (l2n_out), clamped to [0, 1024]: any

@@ -28,6 +28,19 @@
 
 using namespace mib;
 
+// test hook (mibminet_test_xdiv_gpu): xdiv against C division in 64 bits over e0 .. e0 + count - 1;
+// each thread writes its own mismatch count (plain stores, summed on the host)
+__global__ void k_xdiv_check(int d, unsigned m, int xs, long long e0, long long count, unsigned long long* out) {
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x, nt = (long long)gridDim.x * blockDim.x;
+  unsigned long long bad = 0;
+  for (long long i = tid; i < count; i += nt) {
+    const int e = (int)(e0 + i);
+    const long long want = (long long)e / (long long)d;
+    bad += (long long)xdiv(e, m, xs) != (long long)(int)want;
+  }
+  out[tid] = bad;
+}
+
 namespace {
 
 constexpr int MAX_DEVICES = 64;
@@ -53,6 +66,7 @@ struct HostParams {
   int32_t l3_factor = 0, l5_factor = 0;
   bool reorder_bn = true;  // blob flag: -DREORDER_BN variant (canonical) or the plain BN branches
   bool clip_balanced = false;  // blob flag: clip to [-127, 127] (golden model's default; the C clips to -128)
+  bool xr = false;             // set at load: exact integer division at layers 1, 2, 4 (Cfg::XR)
 };
 
 // ---- exact requantisation ------------------------------------------------------------------
@@ -199,6 +213,70 @@ bool choose_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* mbits, 
   return false;
 }
 
+// ---- exact integer division (XR builds) ------------------------------------------------------
+// Parameter sets outside the float envelope above (large folded BN offsets, or factors whose
+// reciprocal window the check cannot prove) run the Cfg::XR kernels, which divide exactly in
+// integers (forward_common.hpp, xdiv): for d != 0 with D = |d| and l = ceil(log2 D),
+// m = ceil(2^(31 + l) / D) lies in [2^31, 2^32), and for every x in [0, 2^31]
+//   floor(x / D) = floor(x m / 2^(31 + l))
+// because x m / 2^(31 + l) = x / D + x e / (D 2^(31 + l)) with e = m D - 2^(31 + l) in [0, D), so
+// the error is below 2^31 D / (D 2^(31 + l)) = 2^-l <= 1 / D, and frac(x / D) <= (D - 1) / D.
+// (Granlund & Montgomery's round-up method with one spare bit of multiplier.)  The device takes
+// x = |e| as a u32 (2^31 for INT_MIN), the 64-bit product x m, its bits 31 .. 62 and a shift by
+// l, then restores the sign of e / d.  xs packs l (bits 0-4) and the sign of d (bit 31).
+struct XDiv {
+  uint32_t m;
+  int32_t xs;
+};
+
+XDiv xdiv_consts(int32_t d) {
+  const uint64_t D = d < 0 ? (uint64_t)(-(int64_t)d) : (uint64_t)d;
+  int l = 0;
+  while (((uint64_t)1 << l) < D) l++;
+  const uint64_t m = (((uint64_t)1 << (31 + l)) + D - 1) / D;
+  return XDiv{(uint32_t)m, (int32_t)((uint32_t)l | (d < 0 ? 0x80000000u : 0u))};
+}
+
+// the device sequence of xdiv on the host (mibminet_test_xdiv)
+int32_t xdiv_host(int32_t e, XDiv c) {
+  const int32_t es = e >> 31;
+  const uint32_t x = (uint32_t)((e ^ es) - es);
+  const uint32_t q = (uint32_t)(((uint64_t)x * c.m) >> 31) >> (c.xs & 31);
+  const int32_t sg = (e ^ c.xs) >> 31;
+  return (int32_t)((q ^ (uint32_t)sg) - (uint32_t)sg);
+}
+
+// Reachable range of an int8 dot product sum_i w[i] x[i] over inputs x in [-128, 127] (every
+// layer entry point takes arbitrary int8 input, and the zero pads lie inside the range).
+struct Range {
+  int64_t lo = 0, hi = 0;
+  int64_t amax() const { return std::max(std::llabs(lo), std::llabs(hi)); }
+};
+Range dot_range(const int8_t* w, int n) {
+  Range r;
+  for (int i = 0; i < n; i++) {
+    r.lo += std::min(-128 * (int64_t)w[i], 127 * (int64_t)w[i]);
+    r.hi += std::max(-128 * (int64_t)w[i], 127 * (int64_t)w[i]);
+  }
+  return r;
+}
+inline bool fits_i32(int64_t v) { return v >= INT32_MIN && v <= INT32_MAX; }
+// the reference's int32 division v / d over v in [lo, hi] is defined (no zero divisor, no
+// INT_MIN / -1) and its operands fit
+inline bool div_ok(Range v, int64_t d) {
+  return d != 0 && fits_i32(v.lo) && fits_i32(v.hi) && !(d == -1 && v.lo == INT32_MIN);
+}
+// REORDER_BN pooled sum of 8: sum_i max(v_i, thr) + off, accumulated in int32 (layer2.c:97-111,
+// layer4.c:99-130): every partial sum and the total must fit
+inline bool pooled_range(Range v, int32_t off, Range* s) {
+  const int64_t thr = -((int64_t)off >> 3);
+  const int64_t mlo = std::max(v.lo, thr), mhi = std::max(v.hi, thr);
+  if (!fits_i32(8 * mlo) || !fits_i32(8 * mhi)) return false;
+  s->lo = 8 * mlo + off;
+  s->hi = 8 * mhi + off;
+  return fits_i32(s->lo) && fits_i32(s->hi);
+}
+
 // ---- blob parsing ------------------------------------------------------------------------
 struct Reader {
   const uint8_t* p;
@@ -286,7 +364,17 @@ int parse_blob(const void* blob, size_t len, HostParams& hp) {
 }
 
 // ---- device parameter image --------------------------------------------------------------
-int build_devparams(const HostParams& hp, DevParams& dp) {
+// Three outcomes per parameter set:
+//  * NET_ERR_RANGE where the reference's own int32 arithmetic is undefined for some input: a zero
+//    divisor (factor, or factor >> 3 in the plain branches), INT_MIN / -1, or an overflowing sum
+//    (acc + off of layer1.c:90-91, the pooled partial sums and sum + off of layer2.c:97-111 /
+//    layer4.c:99-130, the plain layer 4's sum of eight unclipped elements, layer4.c:113-130);
+//  * the float requant kernels (hp.xr = false) when every layer-1, -2 and -4 requant has a proven
+//    float form (choose_reciprocal / choose_floor_form above);
+//  * otherwise the exact-division kernels (hp.xr = true, Cfg::XR: xdiv at layers 1, 2 and 4).
+// Layers 3 and 5 always use the float form (|acc| <= 16 * 128^2 and F2 * T64 * 128^2 + 128, every
+// int32 factor proven: tests/test_requant_exact.py).
+int build_devparams(HostParams& hp, DevParams& dp) {
   const Dims& d = hp.d;
   if (d.F1 != F2 || d.F2 != F2 || d.N != N_OUT) return NET_ERR_UNSUPPORTED;
   if (d.C > 64) return NET_ERR_UNSUPPORTED;
@@ -294,31 +382,113 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
   const int C = d.C, CA = d.C_ALIGN();
   std::memset(&dp, 0, sizeof(dp));
   auto w1 = [&](int f, int c) -> int { return hp.l1_weight_align[(size_t)f * CA + c]; };
-  // value ranges for the float paths (|value| < 2^22 for the magic-offset trick, 2^24 otherwise)
   const int64_t A = 128 * 128;
+  // reachable ranges: e1 = dot + off1 (layer 1); RB: the pooled sums + offset of layers 2 and 4;
+  // plain: the per-element numerators conv + (off >> 3)
+  Range e1[F2], s2[F2], s4[F2];
   for (int f = 0; f < F2; f++) {
-    if (std::llabs((int64_t)hp.l1_offset[f]) + (int64_t)C * A >= (1 << 22)) return NET_ERR_RANGE;
-    if (std::llabs((int64_t)hp.l2_offset[f]) + 8LL * 64 * A >= (1 << 24)) return NET_ERR_RANGE;
-    if (std::llabs((int64_t)hp.l4_offset[f]) + 8LL * F2 * A >= (1 << 24)) return NET_ERR_RANGE;
-  }
-  if (128LL + (int64_t)F2 * d.T64() * A >= (1 << 24)) return NET_ERR_RANGE;
-  if (!hp.reorder_bn) {
-    // plain branches: per-element BN with offset >> 3 and factor >> 3, ReLU right after, in the
-    // floor form (choose_floor_form): the MFMA C-init is the per-filter magic plus the offset
-    // (|x| < 2^22), layer 2's elements clamp to [0, 127], layer 4's to [0, 1024] (anything above
-    // saturates the result)
-    for (int f = 0; f < F2; f++) {
+    const Range r1 = dot_range(&hp.l1_weight_align[(size_t)f * CA], C);
+    const Range r2 = dot_range(&hp.l2_weight_reverse[(size_t)f * 64], 64);
+    const Range r4 = dot_range(&hp.l4_weight[(size_t)f * F2], F2);
+    e1[f].lo = r1.lo + hp.l1_offset[f];
+    e1[f].hi = r1.hi + hp.l1_offset[f];
+    if (!div_ok(e1[f], hp.l1_factor[f])) return NET_ERR_RANGE;
+    if (hp.reorder_bn) {
+      if (!pooled_range(r2, hp.l2_offset[f], &s2[f]) || !div_ok(s2[f], hp.l2_factor[f])) return NET_ERR_RANGE;
+      if (!pooled_range(r4, hp.l4_offset[f], &s4[f]) || !div_ok(s4[f], hp.l4_factor[f])) return NET_ERR_RANGE;
+    } else {
       const int32_t f2 = hp.l2_factor[f] >> 3, o2 = hp.l2_offset[f] >> 3;
       const int32_t f4 = hp.l4_factor[f] >> 3, o4 = hp.l4_offset[f] >> 3;
-      if (f2 == 0 || f4 == 0) return NET_ERR_RANGE;
-      const int64_t v2 = 64LL * A + std::llabs((int64_t)o2), v4 = (int64_t)F2 * A + std::llabs((int64_t)o4);
-      if (v2 >= (1 << 22) || v4 >= (1 << 22)) return NET_ERR_RANGE;
-      int32_t m2, m4;
-      if (!choose_floor_form(f2, 127, v2, &m2, &dp.sp.l2n_r[f], &dp.sp.l2n_c[f])) return NET_ERR_RANGE;
-      if (!choose_floor_form(f4, 1024, v4, &m4, &dp.sp.l4n_r[f], &dp.sp.l4n_c[f])) return NET_ERR_RANGE;
-      dp.sp.l2n_ci[f] = m2 + o2;
-      dp.sp.l4n_ci[f] = m4 + o4;
+      s2[f].lo = r2.lo + o2; s2[f].hi = r2.hi + o2;
+      s4[f].lo = r4.lo + o4; s4[f].hi = r4.hi + o4;
+      if (!div_ok(s2[f], f2) || !div_ok(s4[f], f4)) return NET_ERR_RANGE;
+      // the eight elements max((v + off) / fac, 0) are summed unclipped: trunc is monotone in v
+      const int64_t q4 = std::max({(int64_t)0, s4[f].lo / f4, s4[f].hi / f4});
+      if (!fits_i32(8 * q4)) return NET_ERR_RANGE;
     }
+  }
+  if (hp.l3_factor == 0 || hp.l5_factor == 0) return NET_ERR_RANGE;
+  // Requant constants of layers 1, 2 and 4.  Float forms (xr = false) fail when a range leaves
+  // the float window (|v| < 2^22 for a magic-offset C-init, 2^24 for a converted pooled sum) or a
+  // reciprocal / floor form is not proven; the exact forms (xr = true) always succeed.
+  auto requant = [&](bool xr) -> bool {
+    SmallParams& sp = dp.sp;
+    for (int t = 0; t < P; t++)
+      for (int j = 0; j < 16; j++) {  // N-tile column j: filter 8t + j/2 (P == 2) or j (P == 1)
+        const int f = P == 2 ? 8 * t + (j >> 1) : j;
+        if (xr) {
+          const XDiv x1 = xdiv_consts(hp.l1_factor[f]);
+          dp.l1_cinit[t][j] = hp.l1_offset[f];
+          dp.l1_m[t][j] = x1.m;
+          dp.l1_xs[t][j] = x1.xs;
+        } else {
+          dp.l1_cinit[t][j] = hp.l1_offset[f] + FMAGIC_I;
+          if (e1[f].amax() >= (1 << 22) ||
+              !choose_reciprocal(hp.l1_factor[f], &dp.l1_r[t][j], &dp.l1_c[t][j], 128, e1[f].amax()))
+            return false;
+        }
+      }
+    for (int f = 0; f < F2; f++) {
+      if (hp.reorder_bn) {
+        // biased relu pooling (forward_common.hpp, pool8b): thr = -(off >> 3) (layer2.c:97-111),
+        // clamped to the conv range (|v| <= 64 * 128^2 = 2^20 in layer 2, 16 * 128^2 = 2^18 in
+        // layer 4): at or past either end max(v, thr) - thr is the same for every reachable v
+        // once the offset term off + 8 thr follows the clamped thr
+        const int64_t t2 = std::min<int64_t>(std::max<int64_t>(-((int64_t)hp.l2_offset[f] >> 3), -(1 << 20)), 1 << 20);
+        const int64_t t4 = std::min<int64_t>(std::max<int64_t>(-((int64_t)hp.l4_offset[f] >> 3), -(1 << 18)), 1 << 18);
+        dp.l2_thrb[f] = pbias(f & 1) + (int32_t)t2;  // the wave's filter slot f & 1 (forward_wg.hpp, layer2)
+        dp.l2_offm[f] = (int32_t)(uint32_t)((int64_t)hp.l2_offset[f] + 8 * t2);  // the pooled sums wrap mod 2^32
+        sp.l4_thr[f] = (int32_t)t4;
+        sp.l4_offm[f] = (int32_t)(uint32_t)((int64_t)hp.l4_offset[f] + 8 * t4);
+        int32_t rbits = 0, xs2 = 0;
+        if (xr) {
+          const XDiv x2 = xdiv_consts(hp.l2_factor[f]), x4 = xdiv_consts(hp.l4_factor[f]);
+          dp.l2_m[f] = x2.m;
+          sp.l2_xs[f] = x2.xs;
+          sp.l4_m[f] = x4.m;
+          sp.l4_xs[f] = x4.xs;
+          rbits = (int32_t)x2.m;
+          xs2 = x2.xs;
+        } else {
+          if (s2[f].amax() >= (1 << 24) || s4[f].amax() >= (1 << 24)) return false;
+          if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f], nullptr, 128, s2[f].amax()) ||
+              !choose_reciprocal(hp.l4_factor[f], &sp.l4_r[f], nullptr, 128, s4[f].amax()))
+            return false;
+          std::memcpy(&rbits, &dp.l2_r[f], 4);
+        }
+        sp.l2_tpar[f] = (v4i){PBIAS_TAIL + (int32_t)t2, dp.l2_offm[f], rbits, xs2};
+      } else {
+        // plain branches: per-element BN with offset >> 3 and factor >> 3, ReLU right after.  Float:
+        // the floor form (choose_floor_form), MFMA C-init = per-filter magic plus the offset
+        // (|x| < 2^22); layer 2's elements clamp to [0, 127], layer 4's to [0, 1024] (anything
+        // above saturates the result).  Exact: C-init = the offset, each element xdiv and a clamp.
+        const int32_t f2 = hp.l2_factor[f] >> 3, o2 = hp.l2_offset[f] >> 3;
+        const int32_t f4 = hp.l4_factor[f] >> 3, o4 = hp.l4_offset[f] >> 3;
+        if (xr) {
+          const XDiv x2 = xdiv_consts(f2), x4 = xdiv_consts(f4);
+          sp.l2n_ci[f] = o2;
+          sp.l2n_m[f] = x2.m;
+          sp.l2_xs[f] = x2.xs;
+          sp.l4n_ci[f] = o4;
+          sp.l4n_m[f] = x4.m;
+          sp.l4_xs[f] = x4.xs;
+        } else {
+          int32_t m2, m4;
+          if (s2[f].amax() >= (1 << 22) || s4[f].amax() >= (1 << 22)) return false;
+          if (!choose_floor_form(f2, 127, s2[f].amax(), &m2, &sp.l2n_r[f], &sp.l2n_c[f]) ||
+              !choose_floor_form(f4, 1024, s4[f].amax(), &m4, &sp.l4n_r[f], &sp.l4n_c[f]))
+            return false;
+          sp.l2n_ci[f] = m2 + o2;
+          sp.l4n_ci[f] = m4 + o4;
+        }
+      }
+    }
+    return true;
+  };
+  hp.xr = !requant(false);
+  if (hp.xr) {
+    std::memset(&dp, 0, sizeof(dp));
+    (void)requant(true);
   }
   // layer 1: B operand (column j of N-tile t: filter 8t + j/2, parity j&1 when P == 2)
   for (int t = 0; t < P; t++) {
@@ -342,12 +512,6 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
         bytes[jj] = (int8_t)((c < C && pk == p) ? w1(f, c) : 0);
       }
       std::memcpy(&dp.l1_wfrag_ct[t][lane], bytes, 16);
-    }
-    for (int j = 0; j < 16; j++) {
-      const int f = P == 2 ? 8 * t + (j >> 1) : j;
-      dp.l1_cinit[t][j] = hp.l1_offset[f] + FMAGIC_I;
-      const int64_t v1 = (int64_t)C * A + std::llabs((int64_t)hp.l1_offset[f]);  // |dot + off|
-      if (!choose_reciprocal(hp.l1_factor[f], &dp.l1_r[t][j], &dp.l1_c[t][j], 128, v1)) return NET_ERR_RANGE;
     }
   }
   // layer 2: A operand = banded weights; row i <-> shift n(i) so that lane (c, h) register r
@@ -392,19 +556,6 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
   };
   l2_bands(P, dp.l2_afrag);
   l2_tail_bands(P, dp.l2t_afrag);
-  for (int f = 0; f < F2; f++) {
-    // pooling in the biased relu form (forward_common.hpp, pool8): thr = -(off >> 3) (layer2.c)
-    const int32_t thr2 = -(hp.l2_offset[f] >> 3);
-    dp.l2_thrb[f] = pbias(f & 1) + thr2;  // the wave's filter slot f & 1 (forward_wg.hpp, layer2)
-    dp.l2_offm[f] = hp.l2_offset[f] + 8 * thr2;
-    // pooled sum + offset lies in [0, 8 * 64 * A + |off|] (8 * (off >> 3) <= off)
-    const int64_t v2 = 8LL * 64 * A + std::llabs((int64_t)hp.l2_offset[f]);
-    if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f], nullptr, 128, v2)) return NET_ERR_RANGE;
-    int32_t rbits;
-    std::memcpy(&rbits, &dp.l2_r[f], 4);
-    dp.sp.l2_tpar[f] = (v4i){PBIAS_TAIL + thr2, dp.l2_offm[f], rbits, 0};
-
-  }
   SmallParams& sp = dp.sp;
   // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed.  A
   // operand of MFMA i32_16x16x64_i8 (forward_wg.hpp, layer3): row r, K-slot k of filter f's half
@@ -438,12 +589,6 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
     if ((k >> 4) == hh) std::memcpy(bytes, &hp.l4_weight[(size_t)(k & 15) * F2], 16);
     std::memcpy(&dp.sp.l4_bfrag[lane], bytes, 16);
   }
-  for (int k = 0; k < F2; k++) {
-    sp.l4_thr[k] = -(hp.l4_offset[k] >> 3);
-    sp.l4_offm[k] = hp.l4_offset[k] + 8 * sp.l4_thr[k];  // biased relu pooling (forward_wg.hpp, l4_out)
-    const int64_t v4 = 8LL * F2 * A + std::llabs((int64_t)hp.l4_offset[k]);
-    if (!choose_reciprocal(hp.l4_factor[k], &sp.l4_r[k], nullptr, 128, v4)) return NET_ERR_RANGE;
-  }
   const int T64 = d.T64(), T64A = d.T64_ALIGN();
   if (F2 * T64A / 4 > ND5_MAX) return NET_ERR_UNSUPPORTED;
   for (int n = 0; n < N_OUT; n++) {
@@ -459,11 +604,13 @@ int build_devparams(const HostParams& hp, DevParams& dp) {
 // ---- compiled configurations --------------------------------------------------------------
 // Three shapes: 22 x 1125 (BCI-IV-2a: configs A, B, D, E), 64 x 1000 (config C) and 64 x 480 (the
 // reference's PhysioNet MMMI edgeEEGNet, QuantLab/PhysionetMMMI/config_INQ.json), each compiled
-// with and without -DREORDER_BN and with both clip modes: wg::Cfg<C, T, RB, CB>.
+// with and without -DREORDER_BN, with both clip modes and with float or exact requant:
+// wg::Cfg<C, T, RB, CB, CT, FQ, XR>.
 struct Variant {
   int shape = -1;  // 0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480, -1: unsupported
   bool rb = true;  // -DREORDER_BN branches (canonical)
   bool cb = false; // golden-model clip_balanced (clip to [-127, 127])
+  bool xr = false; // exact integer division (parameters outside the float requant envelope)
   bool ok() const { return shape >= 0; }
 };
 
@@ -475,13 +622,19 @@ Variant variant_of(const HostParams& hp) {
   else if (d.C == 64 && d.T == 480) v.shape = 2;
   v.rb = hp.reorder_bn;
   v.cb = hp.clip_balanced;
+  v.xr = hp.xr;
   return v;
+}
+
+template <int C, int T, bool CT, bool FQ, bool XR, class F>
+int with_variant_x(const Variant& v, F&& f) {
+  if (v.rb) return v.cb ? f(wg::Cfg<C, T, true, true, CT, FQ, XR>{}) : f(wg::Cfg<C, T, true, false, CT, FQ, XR>{});
+  return v.cb ? f(wg::Cfg<C, T, false, true, CT, FQ, XR>{}) : f(wg::Cfg<C, T, false, false, CT, FQ, XR>{});
 }
 
 template <int C, int T, bool CT, bool FQ, class F>
 int with_variant(const Variant& v, F&& f) {
-  if (v.rb) return v.cb ? f(wg::Cfg<C, T, true, true, CT, FQ>{}) : f(wg::Cfg<C, T, true, false, CT, FQ>{});
-  return v.cb ? f(wg::Cfg<C, T, false, true, CT, FQ>{}) : f(wg::Cfg<C, T, false, false, CT, FQ>{});
+  return v.xr ? with_variant_x<C, T, CT, FQ, true>(v, f) : with_variant_x<C, T, CT, FQ, false>(v, f);
 }
 
 // Calls f(K{}) with the kernel configuration K of the variant (CT: channel-major input trials;
@@ -875,7 +1028,7 @@ const char* net_error_string(int code) {
     case NET_ERR_NO_PARAMS: return "no parameters loaded";
     case NET_ERR_UNSUPPORTED: return "unsupported network configuration";
     case NET_ERR_BLOB: return "malformed parameter blob";
-    case NET_ERR_RANGE: return "parameters outside the exact requantisation envelope";
+    case NET_ERR_RANGE: return "value outside the defined range (the reference's int32 arithmetic overflows or divides by zero on these parameters, or a float-input scale outside [2^-60, 2^60])";
     default:
       if (code <= NET_ERR_HIP) return hipGetErrorString((hipError_t)(NET_ERR_HIP - code));
       return "unknown error";
@@ -1077,6 +1230,42 @@ int mibminet_test_upload_stats(int64_t* uploads, int64_t* uploads_while_enqueuei
   return NET_OK;
 }
 
+int mibminet_test_xdiv_host(const int32_t* e, size_t n, int32_t d, int32_t* q) {
+  if ((!e || !q) && n) return NET_ERR_INVALID;
+  if (d == 0) return NET_ERR_INVALID;
+  const XDiv c = xdiv_consts(d);
+  for (size_t i = 0; i < n; i++) q[i] = xdiv_host(e[i], c);
+  return NET_OK;
+}
+
+int mibminet_test_xdiv_gpu(int32_t d, int64_t e0, int64_t count, int64_t* mismatches, int device) {
+  if (!mismatches || d == 0 || count < 0 || e0 < INT32_MIN || e0 + count - 1 > INT32_MAX) return NET_ERR_INVALID;
+  if (const int rc = check_device(device)) return rc;
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
+  constexpr int GRID = 2048, THREADS = 256;
+  unsigned long long* dn = nullptr;
+  hipError_t e = hipMalloc((void**)&dn, sizeof(unsigned long long) * GRID * THREADS);
+  if (e != hipSuccess) return hip_err(e);
+  const XDiv c = xdiv_consts(d);
+  hipLaunchKernelGGL(k_xdiv_check, dim3(GRID), dim3(THREADS), 0, nullptr, d, c.m, c.xs, (long long)e0, (long long)count, dn);
+  e = hipGetLastError();
+  std::vector<unsigned long long> h((size_t)GRID * THREADS);
+  if (e == hipSuccess) e = hipMemcpy(h.data(), dn, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost);
+  (void)hipFree(dn);
+  if (e != hipSuccess) return hip_err(e);
+  int64_t n = 0;
+  for (unsigned long long v : h) n += (int64_t)v;
+  *mismatches = n;
+  return NET_OK;
+}
+
+int mibminet_test_params_xr(void) {
+  Snapshot s = snapshot();
+  if (!s.host) return NET_ERR_NO_PARAMS;
+  return s.host->xr ? 1 : 0;
+}
+
 int mibminet_test_device_images(int device) {
   if (device < 0 || device >= MAX_DEVICES) return NET_ERR_INVALID;
   DeviceState& ds = g_devs[device];
@@ -1127,6 +1316,14 @@ int net_model_compute_batch_multi_ct(int ndev, const int* devices, const int8_t*
 
 int net_model_compute_batch(const int8_t* x, int8_t* y, size_t B, int device) {
   int rc = net_model_compute_batch_async(x, y, B, device, nullptr);
+  if (rc) return rc;
+  DeviceGuard guard(device);
+  if (guard.err != hipSuccess) return hip_err(guard.err);
+  return hip_err(hipStreamSynchronize(nullptr));
+}
+
+int net_model_compute_batch_ct_sync(const int8_t* x, int8_t* y, size_t B, int device) {
+  int rc = net_model_compute_batch_ct(x, y, B, device, nullptr);
   if (rc) return rc;
   DeviceGuard guard(device);
   if (guard.err != hipSuccess) return hip_err(guard.err);

@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
     "net_pack_trials_i8", "net_model_compute_batch_multi", "net_model_compute_batch_ct",
     "net_model_compute_batch_multi_ct", "net_launch_info_ct", "net_model_compute_batch_f32",
+    "net_model_compute_batch_ct_sync",
 )
 
 
@@ -111,6 +112,15 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_model_compute_batch_ct.restype = i
     L.net_model_compute_batch_multi_ct.argtypes = [i, vp, vp, vp, vp, vp]
     L.net_model_compute_batch_multi_ct.restype = i
+    L.net_model_compute_batch_ct_sync.argtypes = [vp, vp, sz, i]
+    L.net_model_compute_batch_ct_sync.restype = i
+    # test hooks (include/mibminet_testing.h)
+    L.mibminet_test_xdiv_host.argtypes = [vp, sz, ctypes.c_int32, vp]
+    L.mibminet_test_xdiv_host.restype = i
+    L.mibminet_test_xdiv_gpu.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, vp, i]
+    L.mibminet_test_xdiv_gpu.restype = i
+    L.mibminet_test_params_xr.argtypes = []
+    L.mibminet_test_params_xr.restype = i
     _lib = L
     return L
 
@@ -237,6 +247,36 @@ def model_compute_batch(x_ptr: int, y_ptr: int, B: int, device: int = 0, stream:
         _check(L.net_model_compute_batch_async(x_ptr, y_ptr, B, device, stream), "net_model_compute_batch_async")
 
 
+def model_compute_batch_ct_sync(x_ptr: int, y_ptr: int, B: int, device: int = 0) -> None:
+    """net_model_compute_batch_ct_sync (SURVEY §8(b)'s signature): channel-major [B][C][T] int8
+    trials and [B][N] logits, device pointers; waits for completion."""
+    _check(load().net_model_compute_batch_ct_sync(x_ptr, y_ptr, B, device), "net_model_compute_batch_ct_sync")
+
+
+def params_exact_division() -> bool:
+    """True when the loaded set runs the exact integer-division kernels (Cfg::XR: a set outside the
+    float requant envelope), False for the float-requant kernels."""
+    rc = load().mibminet_test_params_xr()
+    if rc < 0:
+        raise NetError(rc, "mibminet_test_params_xr")
+    return bool(rc)
+
+
+def xdiv_host(e: np.ndarray, d: int) -> np.ndarray:
+    """The exact-division kernels' integer division emulated on the host (mibminet_test_xdiv_host)."""
+    e = np.ascontiguousarray(e, dtype=np.int32)
+    q = np.empty_like(e)
+    _check(load().mibminet_test_xdiv_host(e.ctypes.data, e.size, int(d), q.ctypes.data), "mibminet_test_xdiv_host")
+    return q
+
+
+def xdiv_gpu_mismatches(d: int, e0: int, count: int, device: int = 0) -> int:
+    """The device xdiv over e0 .. e0 + count - 1 against C division (mibminet_test_xdiv_gpu)."""
+    n = ctypes.c_int64(0)
+    _check(load().mibminet_test_xdiv_gpu(int(d), int(e0), int(count), ctypes.byref(n), device), "mibminet_test_xdiv_gpu")
+    return int(n.value)
+
+
 def launch_info(B: int, device: int = 0, channel_major: bool = False) -> dict:
     arr = (ctypes.c_int32 * 3)()
     fn = load().net_launch_info_ct if channel_major else load().net_launch_info
@@ -344,6 +384,20 @@ def pack_trials_torch(x, stream=None):
     return y
 
 
+def check_trials(x, channel_major: bool) -> None:
+    """Raises ValueError unless ``x`` (NumPy array or torch tensor) is a C-contiguous int8 batch of
+    trials in the chosen layout (check_trial_shape).  The C ABI sees only pointers and counts, so a
+    batch of another element type (e.g. int64 from rng.integers) or with strides would otherwise
+    run and its bytes be read as int8 trials."""
+    dt = str(getattr(x, "dtype", ""))
+    if dt not in ("int8", "torch.int8"):
+        raise ValueError(f"trials must be int8, got {dt or type(x).__name__}")
+    contiguous = x.is_contiguous() if hasattr(x, "is_contiguous") else bool(x.flags["C_CONTIGUOUS"])
+    if not contiguous:
+        raise ValueError("trials must be C-contiguous")
+    check_trial_shape(tuple(x.shape), channel_major)
+
+
 def check_trial_shape(shape, channel_major: bool) -> None:
     """Raises ValueError unless ``shape`` is a batch of trials in the chosen layout: [B][C][T]
     (channel-major) or [B][trial_stride] (time-major).  The C ABI sees only pointers and counts, so
@@ -364,7 +418,7 @@ def model_compute_batch_multi(xs, ys, devices, channel_major: bool = False) -> N
         raise ValueError("xs, ys and devices must have the same length")
     d = _dims()
     for x, y in zip(xs, ys):
-        check_trial_shape(tuple(x.shape), channel_major)
+        check_trials(x, channel_major)
         if tuple(y.shape) != (x.shape[0], d.N):
             raise ValueError(f"logits must be [B][{d.N}] per shard, got {tuple(y.shape)}")
     dev = (ctypes.c_int * n)(*devices)

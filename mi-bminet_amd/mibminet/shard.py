@@ -81,7 +81,7 @@ def forward_devices(x_global, devices, channel_major: bool = False):
     from . import lib
 
     world = len(devices)
-    lib.check_trial_shape(tuple(x_global.shape), channel_major)  # before any device work
+    lib.check_trials(x_global, channel_major)  # before any device work
     xs, ys = [], []
     n_out = lib._dims().N
     for r, d in enumerate(devices):

@@ -84,6 +84,13 @@ def main(out=OUT):
     ps = ParamSet.from_quantlab(net, cfg)
     x = np.concatenate([x0[None], rng.integers(-60, 60, size=(3, 22, 1125))])
     make("appb", ps, x, out=out)
+    # config B's shape with factors and offsets far outside the float requant envelope (offsets
+    # near +-2^30, factors 1 and +-(2^31 - 1), threshold-suppressed filters, |offsets| past 2^22):
+    # the exact-division kernels (Cfg::XR); full int8 range and the reference test range
+    ps = ParamSet.synthetic_extreme(seed=15, C=22, T=1125)
+    x = rng.integers(-128, 128, size=(5, 22, 1125))
+    x[3:] = rng.integers(-60, 60, size=(2, 22, 1125))
+    make("xr22", ps, x, out=out)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,152 @@
+"""Exact-division mode selection on the host (no GPU): which parameter sets run the float requant
+kernels, which the exact-division kernels (Cfg::XR), and which the loader refuses because the
+reference's own int32 arithmetic is undefined on them (overflow, zero divisor, INT_MIN / -1).
+
+The boundaries are recomputed here from the reference's evaluation order (layer1.c:90-91,
+layer2.c:97-111, layer4.c:99-138) with Python integers, independently of the loader's C++.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+from mibminet import lib
+from mibminet.params import HEADER_SIZE, ParamSet, appendix_b_net, dot_ranges, tdiv
+
+I32_MIN, I32_MAX = -(2 ** 31), 2 ** 31 - 1
+
+
+def _load(ps):
+    L = lib.load()
+    b = ps.to_blob()
+    rc = L.net_params_load(b, len(b))
+    if rc == 0:
+        lib._loaded = ps
+        return rc, lib.params_exact_division()
+    return rc, None
+
+
+@pytest.fixture(autouse=True)
+def _unload():
+    yield
+    lib.params_unload()
+
+
+def test_xdiv_host_matches_c_division():
+    """The exact-division sequence (emulated on the host) against C division: every divisor class
+    (+-1, powers of two and their neighbours, int32 extremes, random), dividends around every
+    quotient step of the clipped range and at the int32 ends."""
+    rng = np.random.default_rng(2)
+    ds = [1, -1, 2, -2, 3, 7, 128, -129, 1 << 16, (1 << 16) + 1, (1 << 24) - 1, 1 << 24, 1 << 30, I32_MAX,
+          -I32_MAX, I32_MIN] + [int(v) for v in rng.integers(I32_MIN, I32_MAX, 300) if v]
+    for d in ds:
+        ks = np.arange(-131, 132, dtype=np.int64)
+        e = np.concatenate([(ks[:, None] * d + np.arange(-2, 3)[None, :]).ravel(),
+                            rng.integers(I32_MIN, I32_MAX + 1, 4000), [I32_MIN, I32_MIN + 1, -1, 0, 1, I32_MAX]])
+        e = e[(e >= I32_MIN) & (e <= I32_MAX)]
+        if d == -1:
+            e = e[e != I32_MIN]
+        got = lib.xdiv_host(e.astype(np.int32), d).astype(np.int64)
+        want = np.array([tdiv(int(v), d) for v in e], np.int64)
+        assert np.array_equal(got, want), d
+
+
+def test_calibrated_sets_stay_on_the_float_kernels():
+    """The benchmark and parity sets keep today's float requant kernels."""
+    for seed in range(12):
+        for kw in (dict(), dict(stress=True), dict(C=64, T=1000), dict(weight_bits=4), dict(reorder_bn=False),
+                   dict(clip_balanced=True), dict(C=64, T=480, reorder_bn=False)):
+            rc, xr = _load(ParamSet.synthetic(seed=seed, **kw))
+            assert rc == 0 and xr is False, (seed, kw)
+    net, cfg, _ = appendix_b_net(0)
+    assert _load(ParamSet.from_quantlab(net, cfg)) == (0, False)
+
+
+def test_extreme_sets_load_exact():
+    for rb in (True, False):
+        for C, T in ((22, 1125), (64, 1000), (64, 480)):
+            assert _load(ParamSet.synthetic_extreme(5, C=C, T=T, reorder_bn=rb)) == (0, True), (rb, C, T)
+
+
+@pytest.mark.parametrize("f", [0, 5, 13])
+def test_layer1_boundaries(f):
+    """Layer 1 (acc + off, layer1.c:90-91): the float envelope ends where |dot + off| reaches 2^22
+    (then the exact kernels), and the loader refuses exactly where the int32 sum can overflow."""
+    ps0 = ParamSet.synthetic(seed=2)
+    lo, hi = dot_ranges(ps0)[0][f]
+
+    def at(off, fac=None):
+        ps = ParamSet.synthetic(seed=2)
+        ps.l1_offset[f] = off
+        if fac is not None:
+            ps.l1_factor[f] = fac
+        return _load(ps)
+
+    assert at((1 << 22) - 1 - hi) == (0, False)
+    assert at((1 << 22) - hi) == (0, True)
+    assert at(-(1 << 22) + 1 - lo) == (0, False)
+    assert at(-(1 << 22) - lo) == (0, True)
+    assert at(I32_MAX - hi) == (0, True)
+    assert at(I32_MAX - hi + 1)[0] == lib.NET_ERR_RANGE
+    assert at(I32_MIN - lo) == (0, True)
+    assert at(I32_MIN - lo - 1)[0] == lib.NET_ERR_RANGE
+    # INT_MIN reachable: / -1 is undefined in C, / -2 is not
+    assert at(I32_MIN - lo, -1)[0] == lib.NET_ERR_RANGE
+    assert at(I32_MIN - lo, -2) == (0, True)
+
+
+@pytest.mark.parametrize("name,f", [("l2", 3), ("l4", 9)])
+def test_pooled_boundaries(name, f):
+    """REORDER_BN layers 2 and 4 (sum_8 max(v, -(off >> 3)) + off, layer2.c:97-111): float while
+    the pooled sum stays below 2^24, exact beyond, refused where a partial sum or sum + off leaves
+    int32 (off = -2^31: eight thresholds of 2^28)."""
+    ps0 = ParamSet.synthetic(seed=4)
+    lo, hi = dot_ranges(ps0)[1 if name == "l2" else 2][f]
+
+    def at(off):
+        ps = ParamSet.synthetic(seed=4)
+        getattr(ps, f"{name}_offset")[f] = off
+        return _load(ps)
+
+    assert at((1 << 24) - 1 - 8 * hi) == (0, False)
+    assert at((1 << 24) - 8 * hi) == (0, True)
+    assert at(I32_MAX - 8 * hi) == (0, True)
+    assert at(I32_MAX - 8 * hi + 1)[0] == lib.NET_ERR_RANGE
+    # every element suppressed: sum = 8 thr + off = off & 7, on the float kernels
+    assert at(I32_MIN + 8) == (0, False)
+    assert at(I32_MIN + 15) == (0, False)
+    assert at(I32_MIN)[0] == lib.NET_ERR_RANGE  # 8 * 2^28 overflows
+
+
+def test_plain_layer4_sum_overflow():
+    """Plain layer 4 sums eight unclipped elements (layer4.c:113-130): refused when 8 elements can
+    pass INT32_MAX."""
+    ps0 = ParamSet.synthetic(seed=6, reorder_bn=False)
+    lo, hi = dot_ranges(ps0)[2][2]
+
+    def at(off3):
+        ps = ParamSet.synthetic(seed=6, reorder_bn=False)
+        ps.l4_factor[2] = 8  # factor >> 3 == 1: element = v + (off >> 3)
+        ps.l4_offset[2] = 8 * off3
+        return _load(ps)
+
+    limit = I32_MAX // 8 - hi  # largest off3 with 8 (hi + off3) <= INT32_MAX
+    assert at(limit) == (0, True)
+    assert at(limit + 1)[0] == lib.NET_ERR_RANGE
+
+
+def test_zero_factors_refused():
+    """A zero divisor (C division by zero) is refused; ParamSet refuses to build one, so the blob is
+    patched."""
+    L = lib.load()
+    ps = ParamSet.synthetic(seed=1)
+    blob = bytearray(ps.to_blob())
+    struct.pack_into("<i", blob, HEADER_SIZE + 4 * 3, 0)  # net_l1_factor[3]
+    assert L.net_params_load(bytes(blob), len(blob)) == lib.NET_ERR_RANGE
+    ps = ParamSet.synthetic(seed=1, reorder_bn=False)
+    ps.l2_factor[0] = 8
+    blob = bytearray(ps.to_blob())
+    C_ALIGN = ps.dims.C_ALIGN
+    off = HEADER_SIZE + 2 * 64 + 16 * C_ALIGN  # net_l2_factor[0]
+    struct.pack_into("<i", blob, off, 7)  # 7 >> 3 == 0: the plain branch divides by zero
+    assert L.net_params_load(bytes(blob), len(blob)) == lib.NET_ERR_RANGE
