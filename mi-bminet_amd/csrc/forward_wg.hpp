@@ -539,8 +539,10 @@ __device__ __forceinline__ unsigned lds_addr(const int8_t* p) {
   return (unsigned)(size_t)(const __attribute__((address_space(3))) int8_t*)p;
 }
 __device__ __forceinline__ void dma_b128(Rsrc r, int voff, int soff, unsigned lds) {
-  asm volatile("s_mov_b32 m0, %3\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
-               :: "v"(voff), "s"(r), "s"(soff), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");  // m0: no other user in these kernels (tests/test_mfma_lint.py)
+  // m0 (the LDS base) goes in through an "{m0}" operand: the compiler writes it and knows the asm
+  // reads it, so no value of its own can be kept in m0 across the load
+  asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
+               :: "v"(voff), "s"(r), "s"(soff), "{m0}"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
 }
 
 // Whole-row exchange (K::RX).  Load (m, ph) of wave w: lane L = (h, k) = (L >> 5, L & 31) reads bytes

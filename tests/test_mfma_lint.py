@@ -135,14 +135,17 @@ def test_trial_loop_barriers_do_not_drain_prefetch(device_asm):
         for i in barriers[1:]:
             waits = [l for l in lines[max(0, i - 4):i] if l.startswith("s_waitcnt")]
             assert not waits or "vmcnt" not in waits[-1], (name, lines[i - 4:i + 1])  # the barrier's own wait
-        in_asm = False
-        for i, l in enumerate(lines):
-            if l.startswith(";;#ASMSTART"):
-                in_asm = True
-            elif l.startswith(";;#ASMEND"):
-                in_asm = False
-            elif "m0" in l.split(";")[0].replace(",", " ").split():
-                assert in_asm and l.startswith("s_mov_b32 m0") and " lds" in lines[i + 1], (name, l)
+        code = [l.split(";")[0].strip() for l in lines]
+        for i, l in enumerate(code):
+            ops = l.replace(",", " ").split()
+            if "m0" not in ops:
+                continue
+            # m0 only ever holds the LDS base of the next DMA load: written right before it (the
+            # compiler writes it for the asm's "{m0}" operand), read by nothing else
+            assert ops[1] == "m0" and ops[0].startswith("s_"), (name, l)
+            nxt = next(c for c in code[i + 1:] if c and not c.startswith(".") and "m0" in c.replace(",", " ").split()
+                       or c.endswith(" lds"))
+            assert nxt.startswith("buffer_load_dwordx4") and nxt.endswith(" lds"), (name, l, nxt)
         ct_int8 = _cfg(name)[4:6] == (1, 0) and "CfgILi22E" in name  # Cfg<22, T, RB, CB, CT = true, FQ = false, XR>
         dma = sum(1 for l in lines if l.startswith("buffer_load_dwordx4") and l.endswith(" lds"))
         assert (dma > 0) == ct_int8, (name, dma)
