@@ -55,6 +55,12 @@ int mibminet_test_device_images(int device);
 int mibminet_test_xdiv_host(const int32_t* e, size_t n, int32_t d, int32_t* q);
 int mibminet_test_xdiv_gpu(int32_t d, int64_t e0, int64_t count, int64_t* mismatches, int device);
 
+/* The REORDER_BN pooling constants of layer 2 or 4 for offset `off`: the threshold as the kernels
+ * use it (thr = -(off >> 3) clamped to the layer's conv range [-V, V], V = 2^20 / 2^18) and the
+ * offset term, so that sum_8 max(v - thr_c, 0) + offm (mod 2^32) = sum_8 max(v, thr) + off for
+ * every reachable v. */
+int mibminet_test_pool_consts(int32_t off, int32_t layer, int32_t* thr, int32_t* offm);
+
 /* 1 when the loaded parameter set runs the exact-division kernels, 0 when the float requant
  * kernels, NET_ERR_NO_PARAMS when none is loaded. */
 int mibminet_test_params_xr(void);

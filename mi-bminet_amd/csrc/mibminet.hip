@@ -277,6 +277,14 @@ inline bool pooled_range(Range v, int32_t off, Range* s) {
   return fits_i32(s->lo) && fits_i32(s->hi);
 }
 
+// REORDER_BN pooling constants (build_devparams, requant): the threshold clamped to [-V, V] and the
+// offset term off + 8 max(thr, -V), thr = -(off >> 3).
+void pool_consts(int32_t off, int64_t V, int32_t* thr_c, int32_t* offm) {
+  const int64_t thr = -((int64_t)off >> 3);
+  *thr_c = (int32_t)std::min(std::max(thr, -V), V);
+  *offm = (int32_t)(uint32_t)((int64_t)off + 8 * std::max(thr, -V));  // the pooled sums wrap mod 2^32
+}
+
 // ---- blob parsing ------------------------------------------------------------------------
 struct Reader {
   const uint8_t* p;
@@ -430,16 +438,18 @@ int build_devparams(HostParams& hp, DevParams& dp) {
       }
     for (int f = 0; f < F2; f++) {
       if (hp.reorder_bn) {
-        // biased relu pooling (forward_common.hpp, pool8b): thr = -(off >> 3) (layer2.c:97-111),
-        // clamped to the conv range (|v| <= 64 * 128^2 = 2^20 in layer 2, 16 * 128^2 = 2^18 in
-        // layer 4): at or past either end max(v, thr) - thr is the same for every reachable v
-        // once the offset term off + 8 thr follows the clamped thr
-        const int64_t t2 = std::min<int64_t>(std::max<int64_t>(-((int64_t)hp.l2_offset[f] >> 3), -(1 << 20)), 1 << 20);
-        const int64_t t4 = std::min<int64_t>(std::max<int64_t>(-((int64_t)hp.l4_offset[f] >> 3), -(1 << 18)), 1 << 18);
-        dp.l2_thrb[f] = pbias(f & 1) + (int32_t)t2;  // the wave's filter slot f & 1 (forward_wg.hpp, layer2)
-        dp.l2_offm[f] = (int32_t)(uint32_t)((int64_t)hp.l2_offset[f] + 8 * t2);  // the pooled sums wrap mod 2^32
-        sp.l4_thr[f] = (int32_t)t4;
-        sp.l4_offm[f] = (int32_t)(uint32_t)((int64_t)hp.l4_offset[f] + 8 * t4);
+        // biased relu pooling (forward_common.hpp, pool8b): sum_8 max(v, thr) + off =
+        // sum_8 max(v - thr, 0) + (off + 8 thr), thr = -(off >> 3) (layer2.c:97-111), with thr
+        // clamped to the conv range [-V, V] (V = 64 * 128^2 = 2^20 in layer 2, 16 * 128^2 = 2^18 in
+        // layer 4) so that the biased values cannot wrap.  Past the upper end every max(v, thr) is
+        // thr: the relu terms are 0 either way and the offset term keeps the true thr.  Past the
+        // lower end every max(v, thr) is v: with thr' = -V the relu terms are v + V, so the offset
+        // term is off - 8 V.  Hence offm = off + 8 max(thr, -V).
+        int32_t t2, t4;
+        pool_consts(hp.l2_offset[f], 1 << 20, &t2, &dp.l2_offm[f]);
+        pool_consts(hp.l4_offset[f], 1 << 18, &t4, &sp.l4_offm[f]);
+        dp.l2_thrb[f] = pbias(f & 1) + t2;  // the wave's filter slot f & 1 (forward_wg.hpp, layer2)
+        sp.l4_thr[f] = t4;
         int32_t rbits = 0, xs2 = 0;
         if (xr) {
           const XDiv x2 = xdiv_consts(hp.l2_factor[f]), x4 = xdiv_consts(hp.l4_factor[f]);
@@ -456,7 +466,7 @@ int build_devparams(HostParams& hp, DevParams& dp) {
             return false;
           std::memcpy(&rbits, &dp.l2_r[f], 4);
         }
-        sp.l2_tpar[f] = (v4i){PBIAS_TAIL + (int32_t)t2, dp.l2_offm[f], rbits, xs2};
+        sp.l2_tpar[f] = (v4i){PBIAS_TAIL + t2, dp.l2_offm[f], rbits, xs2};
       } else {
         // plain branches: per-element BN with offset >> 3 and factor >> 3, ReLU right after.  Float:
         // the floor form (choose_floor_form), MFMA C-init = per-filter magic plus the offset
@@ -1257,6 +1267,12 @@ int mibminet_test_xdiv_gpu(int32_t d, int64_t e0, int64_t count, int64_t* mismat
   int64_t n = 0;
   for (unsigned long long v : h) n += (int64_t)v;
   *mismatches = n;
+  return NET_OK;
+}
+
+int mibminet_test_pool_consts(int32_t off, int32_t layer, int32_t* thr, int32_t* offm) {
+  if (!thr || !offm || (layer != 2 && layer != 4)) return NET_ERR_INVALID;
+  pool_consts(off, layer == 2 ? (1 << 20) : (1 << 18), thr, offm);
   return NET_OK;
 }
 

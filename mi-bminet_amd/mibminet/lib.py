@@ -119,6 +119,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.mibminet_test_xdiv_host.restype = i
     L.mibminet_test_xdiv_gpu.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, vp, i]
     L.mibminet_test_xdiv_gpu.restype = i
+    L.mibminet_test_pool_consts.argtypes = [ctypes.c_int32, ctypes.c_int32, vp, vp]
+    L.mibminet_test_pool_consts.restype = i
     L.mibminet_test_params_xr.argtypes = []
     L.mibminet_test_params_xr.restype = i
     _lib = L

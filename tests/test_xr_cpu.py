@@ -150,3 +150,30 @@ def test_zero_factors_refused():
     off = HEADER_SIZE + 2 * 64 + 16 * C_ALIGN  # net_l2_factor[0]
     struct.pack_into("<i", blob, off, 7)  # 7 >> 3 == 0: the plain branch divides by zero
     assert L.net_params_load(bytes(blob), len(blob)) == lib.NET_ERR_RANGE
+
+
+def test_pool_constants_keep_the_pooled_sum():
+    """The biased ReLU pooling (forward_common.hpp, pool8b) with the loader's clamped threshold and
+    offset term equals the reference's sum_8 max(v, -(off >> 3)) + off (layer2.c:97-111,
+    layer4.c:99-130) for offsets across the whole int32 range, including thresholds past either
+    end of the conv range (the kernels' biased values must not wrap, so the threshold is clamped)."""
+    import ctypes
+    L = lib.load()
+    rng = np.random.default_rng(8)
+    for layer, V in ((2, 1 << 20), (4, 1 << 18)):
+        vlo = -((V // (128 * 128)) * 128 * 127)  # 64 (16) taps of (-128) x 127
+        offs = [I32_MIN + 8, I32_MIN + 15, -(1 << 30), -8 * V - 64, -8 * V, -8 * V + 8, -1, 0, 7, 8, 8 * V,
+                8 * V + 9, 1 << 30, I32_MAX - 8 * V] + [int(o) for o in rng.integers(I32_MIN + 8, I32_MAX - 8 * V, 200)]
+        thr_c, offm = ctypes.c_int32(), ctypes.c_int32()
+        for off in offs:
+            assert L.mibminet_test_pool_consts(off, layer, ctypes.byref(thr_c), ctypes.byref(offm)) == 0
+            assert -V <= thr_c.value <= V
+            thr = -(off >> 3)
+            for _ in range(20):
+                v = rng.integers(vlo, V + 1, 8)
+                v[: rng.integers(0, 3)] = rng.choice([vlo, V, 0, thr_c.value])
+                want = int(np.maximum(v, thr).sum()) + off
+                if not I32_MIN <= want <= I32_MAX:
+                    continue
+                got = (int(np.maximum(v - thr_c.value, 0).sum()) + offm.value) % (1 << 32)
+                assert (got - (1 << 32) if got > I32_MAX else got) == want, (layer, off, v.tolist())
