@@ -57,6 +57,10 @@ def parse():
                     help="input layout: tc = time-major batched trials [B][stride] (net_model_compute_batch), "
                          "ct = channel-major [B][C][T] (net_model_compute_batch_ct, transposed inside the kernel), "
                          "f32 = float32 EEG [B][C][T] (net_model_compute_batch_f32, quantised inside the kernel)")
+    ap.add_argument("--params", default="synthetic", choices=("synthetic", "extreme"),
+                    help="synthetic: calibrated seeded weights (the benchmark set, float requant kernels); "
+                         "extreme: requant factors and offsets far outside the float envelope "
+                         "(ParamSet.synthetic_extreme, the exact integer-division kernels)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed launches before the warmup steps (GPU clock ramp)")
@@ -207,8 +211,9 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")
 
-    ps = ParamSet.synthetic(seed=a.seed, C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"],
-                            reorder_bn=a.variant != "plain_bn", clip_balanced=a.variant == "clip_balanced")
+    make = ParamSet.synthetic_extreme if a.params == "extreme" else ParamSet.synthetic
+    ps = make(a.seed, C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"],
+              reorder_bn=a.variant != "plain_bn", clip_balanced=a.variant == "clip_balanced")
     lib.params_load(ps)
     stride = lib.trial_stride()
     B = a.batch
@@ -318,14 +323,14 @@ def main():
             # (time-major under the config's key, other input layouts under "<config>_<layout>")
             key = a.config if a.layout == "tc" else f"{a.config}_{a.layout}"
             tc = tj.get("configs", {}).get(key, tj if tj.get("config") == key else {})
-            if tc.get("batch") == B and a.variant == "canonical":
+            if tc.get("batch") == B and a.variant == "canonical" and a.params == "synthetic":
                 traffic = tc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass
         value = world * B * a.steps / elapsed
         out = {
-            "metric": (METRIC if a.config == "b22" and a.variant == "canonical" and a.layout == "tc"
-                       else f"EEG trials/sec ({cfg['name']}, {a.variant} build, "
+            "metric": (METRIC if a.config == "b22" and a.variant == "canonical" and a.layout == "tc" and a.params == "synthetic"
+                       else f"EEG trials/sec ({cfg['name']}, {a.variant} build, {a.params} parameters, "
                             f"{ {'ct': 'channel-major', 'f32': 'float32 channel-major', 'tc': 'time-major'}[a.layout]} "
                             f"input) at batch {B}"),
             "value": value,
@@ -349,9 +354,9 @@ def main():
                        "grid": info["grid"], "threads": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d,FQ=%d,XR=0>>" % (
+                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d,FQ=%d,XR=%d>>" % (
                              cfg["C"], cfg["T"], a.variant != "plain_bn", a.variant == "clip_balanced",
-                             a.layout != "tc", a.layout == "f32"),
+                             a.layout != "tc", a.layout == "f32", lib.params_exact_division()),
                          "avg_kernel_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes_trial * B},
             "cpu_baseline": None,

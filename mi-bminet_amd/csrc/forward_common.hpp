@@ -35,16 +35,16 @@ constexpr int PBIAS_TAIL = pbias(2);
 
 // Diagnostic phase stamps (tools/probe.hip builds with -DMIB_STAMPS; compiled out otherwise).
 #ifdef MIB_STAMPS
-// g_stamps[8 s + i]: phase i cycles summed over flusher slot s (0: wave 0, 1: last wave);
-// [16] s_memtime total, [17] s_memrealtime total, [18] flushers
-__device__ unsigned long long g_stamps[24];
+// g_stamps[8 w + i]: phase i cycles summed over wave w of every workgroup (w < 8);
+// [64] s_memtime total, [65] s_memrealtime total, [66] flushers
+__device__ unsigned long long g_stamps[72];
 #define MIB_STAMP_INIT unsigned long long _st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
   unsigned long long _st_t = __builtin_amdgcn_s_memtime(); \
   const unsigned long long _st_t0 = _st_t, _st_r0 = __builtin_amdgcn_s_memrealtime();
 #define MIB_STAMP(i) { const unsigned long long _t = __builtin_amdgcn_s_memtime(); _st_acc[i] += _t - _st_t; _st_t = _t; }
 #define MIB_STAMP_FLUSH(cond, slot) if (cond) { for (int _i = 0; _i < 8; _i++) atomicAdd(&g_stamps[8 * (slot) + _i], _st_acc[_i]); \
-  atomicAdd(&g_stamps[16], __builtin_amdgcn_s_memtime() - _st_t0); atomicAdd(&g_stamps[17], __builtin_amdgcn_s_memrealtime() - _st_r0); \
-  atomicAdd(&g_stamps[18], 1ull); }
+  atomicAdd(&g_stamps[64], __builtin_amdgcn_s_memtime() - _st_t0); atomicAdd(&g_stamps[65], __builtin_amdgcn_s_memrealtime() - _st_r0); \
+  atomicAdd(&g_stamps[66], 1ull); }
 #else
 #define MIB_STAMP_INIT
 #define MIB_STAMP(i)

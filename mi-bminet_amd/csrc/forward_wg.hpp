@@ -192,6 +192,7 @@ struct Cfg {
   // DMA ring: RS slots of 1 KB per wave (one block image each), every block of the wave
   static constexpr int RS = DMA ? cmin(NBW, (LDS_WG_MAX - OFF_STG) / (NWAVES * 1024)) : 0;
   static constexpr int PFV = DMA ? 0 : RX ? 4 * NPH : PF;  // loads prefetched into VGPRs
+
   static constexpr int LDS = OFF_STG + (DMA ? NWAVES * RS * 1024 : CT ? NWAVES * STG : 0);
   static_assert(!DMA || RS == NBW, "the DMA ring holds every layer-1 block of a wave");
   static_assert(!DMA || LDS <= LDS_WG_MAX, "two workgroups per CU");
@@ -605,9 +606,8 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
   int xo = R.xoff;
   asm volatile("" : "+v"(xo));
   if constexpr (K::DMA) {
-    // ring slots 0 .. RS - 1 by LDS-DMA.  The ring's transposed reads of the trial just computed
-    // have returned (their MFMAs consumed them); the wait makes that explicit for the hardware,
-    // which would otherwise let a DMA write race a read still queued.
+    // ring slots 0 .. RS - 1 by LDS-DMA (the first trial of a workgroup; layer1 refills each slot
+    // for the next trial).  The wait keeps a DMA write from racing an LDS access still queued.
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const unsigned rb = lds_addr(ring);
     const int n = l1_count<K>(wave);  // slots past the wave's blocks stay unfilled (wave-uniform)
@@ -829,7 +829,9 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
   }
   if constexpr (K::DMA) {
     // Channel-major through the LDS-DMA ring: slots 0 .. RS - 1 hold blocks 0 .. RS - 1, filled a
-    // trial ahead (prefetch_l1).  Block i + 1's fragment is read before block i's MFMAs and requant.
+    // trial ahead (the first trial by prefetch_l1; after that, slot i during the previous trial's
+    // layer 1, right after block i's MFMAs).  Block i + 1's fragment is read before block i's MFMAs
+    // and requant.
     const int n = l1_count<K>(wave);
     int8_t* ring = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::RS * 1024;
     // this trial's fill has landed.  Issued after it on the last wave: the previous trial's logits
@@ -873,12 +875,19 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
           } else {
             l1_block<K, false>(a, blk, smem_y1, R, lane);
           }
+          // slot i's fragment is in registers (its MFMAs read it): refill the slot with the next
+          // trial's block i now, while the TA is idle, instead of all five fills after barrier A,
+          // where the waves' fills queue behind one another (same box: -2.5 %; before barrier B:
+          // +8.0 %)
+          int xo = R.xoff;
+          asm volatile("" : "+v"(xo));
+          dma_b128(rnext, xo, 16 * K::P * i, lds_addr(ring) + 1024 * i);
         }
       }
     };
     if (n == K::NBW) blocks(BoolC<true>{});
     else blocks(BoolC<false>{});
-    return;  // the next trial's fill: k_forward, after barrier A
+    return;
   }
   constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
   v4i xa[NX > 0 ? NX : 1];
@@ -1343,7 +1352,6 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     MIB_LOOP_BARRIER();  // A
     // DMA ring: the next trial's fill, off the layer-1 interval (-0.8 % same box); the ring's
     // reads all returned before the barrier
-    if constexpr (K::DMA) prefetch_l1<K>(rn, R, lane, wave, smem + K::OFF_STG + wave * K::RS * 1024);
     MIB_STAMP(1)
     if constexpr (!DIAG_NOL2) layer2<K>(smem + K::OFF_Y1, smem + K::OFF_Y2, sp, R, T, wave, ln);
     // layer 3 of filter f reads only y2 row f, which this wave wrote
@@ -1380,8 +1388,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   }
   // the last fill (of an empty view past the batch) writes LDS: it lands before the wave ends
   if constexpr (K::DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  MIB_STAMP_FLUSH(tid == 0, 0)
-  MIB_STAMP_FLUSH(tid == 64 * (NWAVES - 1), 1)
+  MIB_STAMP_FLUSH(lane == 0, wave)
   MIB_CLOCK_FLUSH
 }
 

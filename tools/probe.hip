@@ -29,27 +29,32 @@ int main(int argc, char** argv) {
   rc = run();
   if (!rc && hipDeviceSynchronize() != hipSuccess) rc = -1;
   if (rc) { printf("run rc %d %s\n", rc, net_error_string(rc)); return 1; }
-  unsigned long long zero[24] = {0};
+  unsigned long long zero[72] = {0};
   hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), zero, sizeof(zero));
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   hipEventRecord(e0, 0);
   for (int i = 0; i < iters; i++) run();
   hipEventRecord(e1, 0); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
-  unsigned long long st[24];
+  unsigned long long st[72];
   hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
   int32_t info[3]; net_launch_info(B, 0, info);
   const char* names[] = {"layer1 work", "barrier A wait", "layer2 work", "layer3 work", "barrier B wait",
                          "layer4 (last wave)", "layer5 (last wave)", "loop top"};
   double trials = (double)B * iters;
   printf("%sB=%zu iters=%d  %.3f ms/launch  grid %d  lds %d\n", ct ? "channel-major " : "", B, iters, ms / iters, info[0], info[2]);
-  printf("  shader clock from s_memtime/s_memrealtime: %.3f GHz\n", 0.1 * (double)st[16] / (double)st[17]);
-  printf("  %-20s %12s %12s   (cycles per trial, summed over the trial's wave)\n", "phase", "wave 0", "last wave");
-  double t0 = 0, t1 = 0;
+  printf("  shader clock from s_memtime/s_memrealtime: %.3f GHz\n", 0.1 * (double)st[64] / (double)st[65]);
+  printf("  %-20s", "phase (cycles/trial)");
+  for (int w = 0; w < 8; w++) printf("  wave %d", w);
+  printf("\n");
+  double tot[8] = {0};
   for (int i = 0; i < 8; i++) {
-    printf("  %-20s %12.0f %12.0f\n", names[i], st[i] / trials, st[8 + i] / trials);
-    t0 += st[i]; t1 += st[8 + i];
+    printf("  %-20s", names[i]);
+    for (int w = 0; w < 8; w++) { printf(" %7.0f", st[8 * w + i] / trials); tot[w] += st[8 * w + i]; }
+    printf("\n");
   }
-  printf("  %-20s %12.0f %12.0f\n", "total", t0 / trials, t1 / trials);
+  printf("  %-20s", "total");
+  for (int w = 0; w < 8; w++) printf(" %7.0f", tot[w] / trials);
+  printf("\n");
   return 0;
 }
