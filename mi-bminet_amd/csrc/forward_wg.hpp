@@ -49,7 +49,8 @@ constexpr int NTHREADS = 64 * NWAVES;
 constexpr int WPE = 4;                // waves per SIMD (two workgroups per CU)
 constexpr int LDS_WG_MAX = 160 * 1024 / 2;  // LDS per workgroup at two workgroups per CU
 constexpr int PF_MAX = 9;             // layer-1 blocks per wave prefetched one trial ahead
-constexpr int PF_MAX_PLAIN = 3;       // plain BN: fewer, no spills (config B -5.4 %, C -13.6 %)
+constexpr int PF_MAX_PLAIN = 3;       // plain BN: fewer, no spills (config B -5.4 %, C -13.6 %; 4, 5
+                                      // measured slower with the LDS-DMA of the rest)
 constexpr int PF_MAX_PLAIN_CT = 2;
 static_assert(FPW == 2, "tail-tile and layer-3 mapping assume two filters per wave");
 // Wave priorities (s_setprio): the last wave's layers 4-5 are the longest dependency chain of the
@@ -173,7 +174,7 @@ struct Cfg {
   // layer 4 reads a row with one (4-byte aligned) ds_read_b128, 2-way at most (3 per trial)
   static constexpr int Y3S = 16;
   static constexpr int T64A = (T64 + 3) & ~3;           // y4 row stride (reference T64_ALIGN)
-  static constexpr bool L4PIPE = P == 2 && RB;          // layer-4 MFMA/pooling overlap (registers)
+  static constexpr bool L4PIPE = P == 2 && RB;  // layer-4 MFMA/pooling overlap (registers)
   static constexpr int ND5 = F2 * T64A / 4;             // layer-5 input dwords
   static constexpr int N5L = (ND5 + 15) / 16;           // layer-5 dwords per lane
   // LDS carve
@@ -192,8 +193,14 @@ struct Cfg {
   // DMA ring: RS slots of 1 KB per wave (one block image each), every block of the wave
   static constexpr int RS = DMA ? cmin(NBW, (LDS_WG_MAX - OFF_STG) / (NWAVES * 1024)) : 0;
   static constexpr int PFV = DMA ? 0 : RX ? 4 * NPH : PF;  // loads prefetched into VGPRs
+  // time-major plain BN (LDMA): the blocks past PF go a trial ahead into an LDS slot per block by
+  // LDS-DMA, where they wait in no register (the VGPR prefetch of all blocks spills; loading them
+  // at the start of their own layer 1 exposes the HBM latency)
+  static constexpr bool LDMA = !CT_ && !RB_ && P == 2 && NBW > PF;
+  static constexpr int NLD = LDMA ? NBW - PF : 0;
 
-  static constexpr int LDS = OFF_STG + (DMA ? NWAVES * RS * 1024 : CT ? NWAVES * STG : 0);
+  static constexpr int LDS = OFF_STG + (DMA ? NWAVES * RS * 1024 : CT ? NWAVES * STG : NWAVES * NLD * 1024);
+  static_assert(!LDMA || LDS <= LDS_WG_MAX, "two workgroups per CU");
   static_assert(!DMA || RS == NBW, "the DMA ring holds every layer-1 block of a wave");
   static_assert(!DMA || LDS <= LDS_WG_MAX, "two workgroups per CU");
   static_assert(C >= 1 && C <= 64, "C must be <= 64 (one 64-byte MFMA K window)");
@@ -598,9 +605,17 @@ __device__ __forceinline__ v4i load_f(Rsrc r, int xoff, int i, int m) {
   return (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xoff + 64 * K::P * i + 16 * m, 0, 0);
 }
 
+// LDS slots of wave `wave` filled by LDS-DMA (K::DMA: the channel-major ring; K::LDMA: the plain
+// build's blocks past PF)
+template <class K>
+__device__ __forceinline__ int8_t* ring_base(int8_t* smem, int wave) {
+  return smem + K::OFF_STG + wave * (K::DMA ? K::RS : K::NLD) * 1024;
+}
+
 template <class K>
 __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, int wave = 0,
-                                            int8_t* ring = nullptr) {
+                                            int8_t* smem = nullptr) {
+  int8_t* ring = (K::DMA || K::LDMA) ? ring_base<K>(smem, wave) : nullptr;
   // laundered: otherwise xoff + 16 GS i is hoisted out of the trial loop into a register per slot
   // instead of riding in the loads' immediate offsets
   int xo = R.xoff;
@@ -631,6 +646,13 @@ __device__ __forceinline__ void prefetch_l1(Rsrc r, Regs<K>& R, int lane = 0, in
       for (int m = 0; m < 4; m++)
         R.pf[4 * ph + m] = (v4i)__builtin_amdgcn_raw_buffer_load_b128(r, xr, 16 * m * K::T + 512 * ph, 0);
     return;
+  }
+  if constexpr (K::LDMA) {
+    // issued before the VGPR loads: the compiler's vmcnt waits for those then also cover these
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slots' reads of this trial have returned
+    const unsigned rb = lds_addr(ring);
+#pragma unroll
+    for (int i = 0; i < K::NLD; i++) dma_b128(r, xo + (K::PF + i) * 16 * K::GS, 0, rb + 1024 * i);
   }
 #pragma unroll
   for (int i = 0; i < K::PF; i++) R.pf[i] = load_a<K>(r, xo, i);
@@ -889,10 +911,19 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
     else blocks(BoolC<false>{});
     return;
   }
-  constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now, consumed last
+  constexpr int NX = K::NBW - K::PF;  // blocks not prefetched: load now (or from the LDS slots), consumed last
   v4i xa[NX > 0 ? NX : 1];
+  if constexpr (K::LDMA) {
+    // the slots were filled before this trial's VGPR prefetch was issued: once all but the last PF
+    // vector-memory operations are done, so are the fills (in-order completion)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(K::PF) : "memory");
+    const int8_t* ring = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::NLD * 1024;
 #pragma unroll
-  for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
+    for (int i = 0; i < NX; i++) xa[i] = *(const v4i*)(ring + 1024 * i + 16 * lane);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NX; i++) xa[i] = load_a<K>(rcur, R.xoff, K::PF + i);
+  }
   const int n = l1_count<K>(wave);
   int8_t* stg = smem_y1 - K::OFF_Y1 + K::OFF_STG + wave * K::STG;  // channel-major staging
   if constexpr (K::RX) {
@@ -988,7 +1019,7 @@ __device__ __forceinline__ void layer1(Rsrc rcur, Rsrc rnext, int8_t* smem_y1, R
       }
     }
   }
-  prefetch_l1<K>(rnext, R);
+  prefetch_l1<K>(rnext, R, lane, wave, smem_y1 - K::OFF_Y1);
 }
 
 // ---- layer 2 ---------------------------------------------------------------------------------
@@ -1320,7 +1351,7 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
   const SmallParams* sp = (const SmallParams*)(smem + K::OFF_SP);
   if ((int)blockIdx.x < B)
     prefetch_l1<K>(trial_rsrc<K>(x + MIB_TRIAL_OFF(blockIdx.x), MIB_TRIALS_LEFT(blockIdx.x), wave), R, lane, wave,
-                   smem + K::OFF_STG + wave * K::RS * 1024);
+                   smem);
   // The first trial's fragments land before its layer 1 starts, as in k_layer (where loads still
   // in flight at layer 1 gave a rare wrong layer-1 row).  Once per workgroup.
   __builtin_amdgcn_s_waitcnt(0);
@@ -1413,7 +1444,7 @@ __global__ __launch_bounds__(NTHREADS) void k_layer(const DevParams* __restrict_
   __syncthreads();
   if (stage == 1) {  // [T][C] packed (XTRIAL bytes) -> [F1][T_ALIGN]
     const Rsrc rin = trial_rsrc<K>(in, 1, wave);
-    prefetch_l1<K>(rin, R, lane, wave);
+    prefetch_l1<K>(rin, R, lane, wave, smem);
     // All fragment loads land before layer 1 starts.  With them still in flight, this single-
     // workgroup path gave a wrong layer-1 row in ~2 % of calls on gfx950 (tools/stress.py; the
     // batched kernel, whose fragments are loaded a whole trial ahead, showed none in 39 M trials).

@@ -125,7 +125,8 @@ def test_trial_loop_barriers_do_not_drain_prefetch(device_asm):
     s_barrier but the one before the loop is preceded by an s_waitcnt on vmcnt.  The channel-major LDS-DMA
     fill is inline asm for this reason: with __builtin_amdgcn_raw_ptr_buffer_load_lds
     the compiler puts vmcnt(0) before every __syncthreads().  The DMA instructions set m0 themselves,
-    and nothing else in these kernels touches m0.  (The DMA ring serves the 22-channel shapes only.)"""
+    and nothing else in these kernels touches m0.  (LDS-DMA serves the 22-channel shapes only: the
+    channel-major int8 ring, and the blocks past the VGPR prefetch of time-major plain BN.)"""
     funcs = {n: ls for n, ls in _functions(device_asm).items() if "k_forward" in n}
     assert len(funcs) == 72
     n_dma = 0
@@ -146,11 +147,19 @@ def test_trial_loop_barriers_do_not_drain_prefetch(device_asm):
             nxt = next(c for c in code[i + 1:] if c and not c.startswith(".") and "m0" in c.replace(",", " ").split()
                        or c.endswith(" lds"))
             assert nxt.startswith("buffer_load_dwordx4") and nxt.endswith(" lds"), (name, l, nxt)
-        ct_int8 = _cfg(name)[4:6] == (1, 0) and "CfgILi22E" in name  # Cfg<22, T, RB, CB, CT = true, FQ = false, XR>
         dma = sum(1 for l in lines if l.startswith("buffer_load_dwordx4") and l.endswith(" lds"))
-        assert (dma > 0) == ct_int8, (name, dma)
+        assert (dma > 0) == (_dma_kind(name) is not None), (name, dma)
         n_dma += dma > 0
-    assert n_dma == 8
+    assert n_dma == 12
+
+
+def _dma_kind(name):
+    """Cfg<C, T, RB, CB, CT, FQ, XR>: "ring" for channel-major int8 22-ch, "ldma" for time-major plain
+    BN 22-ch (int8 input), None for the rest."""
+    c = _cfg(name)
+    if c[0] != 22 or c[5]:
+        return None
+    return "ring" if c[4] else None if c[2] else "ldma"
 
 
 def _cfg(name):
@@ -160,18 +169,21 @@ def _cfg(name):
 
 
 def test_dma_ring_wait_counts_issued_ops(device_asm):
-    """Layer 1 of the DMA kernels waits for the ring fill with a fixed s_waitcnt vmcnt(N) (inline
-    asm, forward_wg.hpp layer1): N = 1 on the last wave, whose previous trial's logits store was
-    issued after the fill and need not complete, 0 elsewhere.  That is only safe while at least N
-    vector-memory operations follow the trial loop's last fill: here, the one logits store
-    (ADVICE r04).  Scratch traffic (spills) after the fill only makes the wait stricter."""
+    """Layer 1 of the LDS-DMA kernels waits for the fill with a fixed s_waitcnt vmcnt(N) (inline asm,
+    forward_wg.hpp layer1).  Channel-major ring: N = 1 on the last wave, whose previous trial's
+    logits store was issued after the fill and need not complete, 0 elsewhere.  Time-major plain BN:
+    N = PF, the VGPR prefetch loads issued right after the LDS-DMA ones.  That is only safe while at
+    least N vector-memory operations follow the trial loop's last fill.  Scratch
+    traffic (spills) after the fill only makes the wait stricter."""
+    import re
     funcs = {n: ls for n, ls in _functions(device_asm).items() if "k_forward" in n}
     checked = 0
     for name, lines in funcs.items():
         fills = [i for i, l in enumerate(lines) if l.startswith("buffer_load_dwordx4") and l.endswith(" lds")]
         if not fills:
             continue
-        head = next(i for i, l in enumerate(lines) if "=>This Loop Header: Depth=1" in l)
+        # the trial loop: the last depth-1 loop header before the last fill
+        head = max(i for i, l in enumerate(lines[:fills[-1]]) if re.search(r"=>This (Inner )?Loop Header: Depth=1", l))
         loop_fills = [i for i in fills if i > head]
         assert loop_fills, name
         waits, in_asm = [], False
@@ -182,12 +194,15 @@ def test_dma_ring_wait_counts_issued_ops(device_asm):
                 in_asm = False
             elif in_asm and i > head and l.startswith("s_waitcnt vmcnt("):
                 waits.append(int(l.split("(")[1].split(")")[0]))
-        loop_waits = [w for w in waits]
-        assert sorted(set(loop_waits)) == [0, 1], (name, loop_waits)
-        after = [l for l in lines[loop_fills[-1] + 1:] if l.startswith(("global_store", "buffer_store", "global_load", "buffer_load"))]
-        assert len([l for l in after if l.startswith("global_store_dword ")]) >= max(loop_waits), (name, after)
+        kind = _dma_kind(name)
+        assert sorted(set(waits)) == ([0, 1] if kind == "ring" else [3]), (name, kind, waits)
+        after = [l for l in lines[loop_fills[-1] + 1:]
+                 if l.startswith(("global_store", "buffer_store", "global_load", "buffer_load")) and not l.endswith(" lds")]
+        if kind == "ring":
+            after = [l for l in after if l.startswith("global_store_dword ")]
+        assert len(after) >= max(waits), (name, after)
         checked += 1
-    assert checked == 8
+    assert checked == 12
 
 
 def test_layer1_cinit_not_written_near_loads(device_asm):
