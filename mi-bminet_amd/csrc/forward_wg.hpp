@@ -114,9 +114,10 @@ struct Cfg {
   static constexpr int NT4 = (8 * T64 + 63) / 64;       // L4 MFMAs of 64 time samples
   static constexpr L1Split SPL = l1_split(NB1);
   static constexpr int NBW = cmax(SPL.cm + (SPL.rm ? 1 : 0), SPL.cl);  // L1 blocks per wave (max)
-  // of which prefetched a trial ahead (the plain-BN builds hold more per-filter state)
+  // of which prefetched a trial ahead (the plain-BN and 22-channel exact-division builds hold more
+  // per-lane state; the rest of their blocks go by LDMA below)
   // (float input: the first block's four 16-byte pieces; the others load one block ahead)
-  static constexpr int PF = FQ_ ? 4 : cmin(NBW, RB ? PF_MAX : CT_ ? PF_MAX_PLAIN_CT : PF_MAX_PLAIN);
+  static constexpr int PF = FQ_ ? 4 : cmin(NBW, RB && !(XR_ && P == 2) ? PF_MAX : CT_ ? PF_MAX_PLAIN_CT : PF_MAX_PLAIN);
   // Channel-major int8, 22 channels, through LDS-DMA (layer1): each block's rows go from HBM straight
   // into an LDS ring with buffer_load_dwordx4 ... lds, a trial ahead, and the A fragments come back
   // with ds_read_b64_tr_b16: no VGPR round trip, no ds_write (RS ring slots, LDS carve below).  The
@@ -193,10 +194,11 @@ struct Cfg {
   // DMA ring: RS slots of 1 KB per wave (one block image each), every block of the wave
   static constexpr int RS = DMA ? cmin(NBW, (LDS_WG_MAX - OFF_STG) / (NWAVES * 1024)) : 0;
   static constexpr int PFV = DMA ? 0 : RX ? 4 * NPH : PF;  // loads prefetched into VGPRs
-  // time-major plain BN (LDMA): the blocks past PF go a trial ahead into an LDS slot per block by
-  // LDS-DMA, where they wait in no register (the VGPR prefetch of all blocks spills; loading them
-  // at the start of their own layer 1 exposes the HBM latency)
-  static constexpr bool LDMA = !CT_ && !RB_ && P == 2 && NBW > PF;
+  // time-major plain BN and exact division, 22 channels (LDMA): the blocks past PF go a trial ahead
+  // into an LDS slot per block by LDS-DMA, where they wait in no register (the VGPR prefetch of all
+  // blocks spills; loading them at the start of their own layer 1 exposes the HBM latency).  XR
+  // config B: 5 VGPR blocks spilled 40-44 bytes; 3 + 2 by DMA, 8 bytes: -17 % same box.
+  static constexpr bool LDMA = !CT_ && (!RB_ || XR_) && P == 2 && NBW > PF;
   static constexpr int NLD = LDMA ? NBW - PF : 0;
 
   static constexpr int LDS = OFF_STG + (DMA ? NWAVES * RS * 1024 : CT ? NWAVES * STG : NWAVES * NLD * 1024);

@@ -126,7 +126,8 @@ def test_trial_loop_barriers_do_not_drain_prefetch(device_asm):
     fill is inline asm for this reason: with __builtin_amdgcn_raw_ptr_buffer_load_lds
     the compiler puts vmcnt(0) before every __syncthreads().  The DMA instructions set m0 themselves,
     and nothing else in these kernels touches m0.  (LDS-DMA serves the 22-channel shapes only: the
-    channel-major int8 ring, and the blocks past the VGPR prefetch of time-major plain BN.)"""
+    channel-major int8 ring, and the blocks past the VGPR prefetch of time-major plain BN and exact
+    division.)"""
     funcs = {n: ls for n, ls in _functions(device_asm).items() if "k_forward" in n}
     assert len(funcs) == 72
     n_dma = 0
@@ -150,16 +151,16 @@ def test_trial_loop_barriers_do_not_drain_prefetch(device_asm):
         dma = sum(1 for l in lines if l.startswith("buffer_load_dwordx4") and l.endswith(" lds"))
         assert (dma > 0) == (_dma_kind(name) is not None), (name, dma)
         n_dma += dma > 0
-    assert n_dma == 12
+    assert n_dma == 14
 
 
 def _dma_kind(name):
     """Cfg<C, T, RB, CB, CT, FQ, XR>: "ring" for channel-major int8 22-ch, "ldma" for time-major plain
-    BN 22-ch (int8 input), None for the rest."""
+    BN or exact-division 22-ch (int8 input), None for the rest."""
     c = _cfg(name)
     if c[0] != 22 or c[5]:
         return None
-    return "ring" if c[4] else None if c[2] else "ldma"
+    return "ring" if c[4] else "ldma" if (not c[2] or c[6]) else None
 
 
 def _cfg(name):
@@ -171,8 +172,8 @@ def _cfg(name):
 def test_dma_ring_wait_counts_issued_ops(device_asm):
     """Layer 1 of the LDS-DMA kernels waits for the fill with a fixed s_waitcnt vmcnt(N) (inline asm,
     forward_wg.hpp layer1).  Channel-major ring: N = 1 on the last wave, whose previous trial's
-    logits store was issued after the fill and need not complete, 0 elsewhere.  Time-major plain BN:
-    N = PF, the VGPR prefetch loads issued right after the LDS-DMA ones.  That is only safe while at
+    logits store was issued after the fill and need not complete, 0 elsewhere.  Time-major plain BN
+    and exact division: N = PF, the VGPR prefetch loads issued right after the LDS-DMA ones.  That is only safe while at
     least N vector-memory operations follow the trial loop's last fill.  Scratch
     traffic (spills) after the fill only makes the wait stricter."""
     import re
@@ -202,7 +203,7 @@ def test_dma_ring_wait_counts_issued_ops(device_asm):
             after = [l for l in after if l.startswith("global_store_dword ")]
         assert len(after) >= max(waits), (name, after)
         checked += 1
-    assert checked == 12
+    assert checked == 14
 
 
 def test_layer1_cinit_not_written_near_loads(device_asm):

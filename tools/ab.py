@@ -30,11 +30,12 @@ def main():
     ap.add_argument("--variant", default="canonical", choices=("canonical", "plain_bn", "clip_balanced"))
     ap.add_argument("--ct", action="store_true", help="channel-major input (net_model_compute_batch_ct)")
     ap.add_argument("--f32", action="store_true", help="float32 channel-major input (net_model_compute_batch_f32)")
+    ap.add_argument("--extreme", action="store_true", help="ParamSet.synthetic_extreme (the exact-division kernels)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     C, T = {"b22": (22, 1125), "c64": (64, 1000), "p64": (64, 480)}[a.cfg]
-    blob = ParamSet.synthetic(seed=1, C=C, T=T, reorder_bn=a.variant != "plain_bn",
-                              clip_balanced=a.variant == "clip_balanced").to_blob()
+    mk = ParamSet.synthetic_extreme if a.extreme else ParamSet.synthetic
+    blob = mk(1, C=C, T=T, reorder_bn=a.variant != "plain_bn", clip_balanced=a.variant == "clip_balanced").to_blob()
     libs = []
     for p in a.libs:
         L = ctypes.CDLL(os.path.abspath(p), mode=ctypes.RTLD_LOCAL)
