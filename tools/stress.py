@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--cfg", default="b22", choices=("b22", "c64", "p64"), help="geometry of the batch stress")
     ap.add_argument("--variants", default="canonical",
                     help="comma list of build variants to stress: canonical, plain_bn, clip_balanced")
+    ap.add_argument("--extreme", action="store_true",
+                    help="ParamSet.synthetic_extreme sets (the exact-division kernels) instead of synthetic")
     a = ap.parse_args()
     if a.lib:
         lib.load(os.path.abspath(a.lib))
@@ -61,11 +63,15 @@ def main():
                 print(f"layer1 call {i}: {nb} bytes differ, first {w[:4].tolist()}", flush=True)
     print(f"layer1: {bad1} of {a.n1} calls wrong ({time.time() - t0:.1f} s)", flush=True)
 
-    modes = [(v, st) for v in a.variants.split(",") for st in (True, False)]
+    modes = [(v, st) for v in a.variants.split(",") for st in ((False,) if a.extreme else (True, False))]
     for variant, stress in modes:
         gC, gT = {"b22": (22, 1125), "c64": (64, 1000), "p64": (64, 480)}[a.cfg]
-        ps = ParamSet.synthetic(seed=7, stress=stress, reorder_bn=variant != "plain_bn",
-                                clip_balanced=variant == "clip_balanced", C=gC, T=gT)
+        if a.extreme:
+            ps = ParamSet.synthetic_extreme(7, reorder_bn=variant != "plain_bn",
+                                            clip_balanced=variant == "clip_balanced", C=gC, T=gT)
+        else:
+            ps = ParamSet.synthetic(seed=7, stress=stress, reorder_bn=variant != "plain_bn",
+                                    clip_balanced=variant == "clip_balanced", C=gC, T=gT)
         lib.params_load(ps)
         stride = lib.trial_stride()
         g = torch.Generator(device="cuda:0").manual_seed(11 + stress)
@@ -116,7 +122,7 @@ def main():
                 if bad2 <= 5:
                     rows = torch.nonzero(bad).flatten()[:4].tolist()
                     print(f"batch launch {i}: {nb} trials differ, first {rows}", flush=True)
-        print(f"batch ({a.layout}, {a.cfg}, {variant}, stress={stress}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
+        print(f"batch ({a.layout}, {a.cfg}, {variant}, {'extreme' if a.extreme else f'stress={stress}'}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
               f"{a.nb * a.B} distinct ({time.time() - t0:.1f} s)", flush=True)
 
 if __name__ == "__main__":
