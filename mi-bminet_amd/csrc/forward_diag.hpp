@@ -9,10 +9,18 @@
 //   MIB_DIAG_NOBAR       no barriers in the trial loop
 //   MIB_DIAG_SAME_TRIAL  every trial reads trial 0 (no HBM traffic after the first)
 //   MIB_DIAG_NOL2 / NOTAIL / NOL3 / NOL45  skip layer 2 / the layer-2 tail / layer 3 / layers 4-5
+//   MIB_DIAG_L2_TWO      layer 2's full tiles run 2 of their 3 MFMAs (the upper bound of a 2:4
+//                        sparse form: two smfmac_32x32x64 in place of three dense 32x32x32)
 #pragma once
 
 namespace mib {
 namespace wg {
+
+#ifdef MIB_DIAG_L2_TWO
+constexpr int DIAG_L2_STEPS = 2;
+#else
+constexpr int DIAG_L2_STEPS = 3;
+#endif
 
 #ifdef MIB_DIAG_NOL2
 constexpr bool DIAG_NOL2 = true;

@@ -68,6 +68,7 @@ constexpr int W45 = 4;
 #ifndef MIB_DIAG
 // Timing-proxy switches (forward_diag.hpp): all off in the library.
 constexpr bool DIAG_NOL2 = false, DIAG_NOTAIL = false, DIAG_NOL3 = false, DIAG_NOL45 = false;
+constexpr int DIAG_L2_STEPS = 3;
 #endif
 
 template <bool V>
@@ -1156,7 +1157,7 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = K::RB ? pbias(fi) : R.thr2[fi];  // plain branch: C-init
 #pragma unroll
-      for (int s = 0; s < 3; s++)
+      for (int s = 0; s < DIAG_L2_STEPS; s++)
         acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(R.af[fi][s], *(const v4i*)(pb + l2_boff<K>(s, 0)), acc, 0, 0, 0);
       // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
       unsigned w;
