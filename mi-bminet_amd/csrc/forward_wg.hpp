@@ -1053,6 +1053,24 @@ __device__ __forceinline__ unsigned floor_sum8(const v16i& acc, float r, float c
   return ((e[0] + e[1] + e[2]) + (e[3] + e[4]) + (e[5] + e[6])) + (e[7] - 8u * (unsigned)FMAGIC_I);
 }
 
+// Plain layer 4's elements have no clip in the reference, only the ReLU: e = max(q, 0) is one
+// full-rate saturating subtract of the floor form's bits, bits(FMAGIC + q) - FMAGIC_I clamped at 0,
+// where layer 2 needs the two-sided fmed3.  The host verifies the form exactly up to the step q = 1024;
+// past it the form is monotone, so a larger element still reads >= 1024, and any element >= 1016
+// already saturates the window's result (sum >> 3 >= 127).  Eight elements below 2^22 sum below 2^25.
+template <int BASE>
+__device__ __forceinline__ unsigned relu_sum8(const v16i& acc, float r, float c) {
+  unsigned e[8];
+#pragma unroll
+  for (int i = 0; i < 8; i += 2) {
+    const f2 q = __builtin_elementwise_fma((f2){__int_as_float(acc[BASE + i]), __int_as_float(acc[BASE + i + 1])},
+                                           (f2){r, r}, (f2){c, c});
+    e[i] = __builtin_elementwise_sub_sat(__float_as_uint(q[0]), (unsigned)FMAGIC_I);
+    e[i + 1] = __builtin_elementwise_sub_sat(__float_as_uint(q[1]), (unsigned)FMAGIC_I);
+  }
+  return ((e[0] + e[1] + e[2]) + (e[3] + e[4])) + ((e[5] + e[6]) + e[7]);
+}
+
 __device__ __forceinline__ unsigned l2n_out(const v16i& acc, float r, float c) {
   const unsigned s0 = floor_sum8<0, 127>(acc, r, c), s1 = floor_sum8<8, 127>(acc, r, c);
   return (s0 >> 3) | ((s1 >> 3) << 8);
@@ -1255,11 +1273,9 @@ __device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* s
     return (unsigned)sm[0] | ((unsigned)sm[1] << 8);
   } else {
     // layer4.c:113-130 without REORDER_BN: element = (dot + off) / factor (no clip), ReLU,
-    // sum of 8, >> 3, clip.  Elements in the floor form (l2n_out), clamped to [0, 1024]: any
-    // element >= 1024 already saturates the result, and the host verified the form up to there.
+    // sum of 8, >> 3, clip.  Elements in the floor form (l2n_out) with the ReLU only (relu_sum8).
     const float rn = MIB_K4(sp->l4n_r, float), cn = MIB_K4(sp->l4n_c, float);
-    const int sm[2] = {min((int)(floor_sum8<0, 1024>(acc, rn, cn) >> 3), 127),
-                       min((int)(floor_sum8<8, 1024>(acc, rn, cn) >> 3), 127)};
+    const int sm[2] = {min((int)(relu_sum8<0>(acc, rn, cn) >> 3), 127), min((int)(relu_sum8<8>(acc, rn, cn) >> 3), 127)};
     return (unsigned)sm[0] | ((unsigned)sm[1] << 8);
   }
 }
