@@ -59,6 +59,25 @@ def test_layer4_elements(fac):
     _check(fac, 1024, 16 * A + 777)
 
 
+@pytest.mark.parametrize("fac", [1, -3, 16, 999, -4096])
+def test_layer4_relu_only_elements(fac):
+    """Plain layer 4 takes only the ReLU of the form, max(bits - bits(K), 0) (forward_wg.hpp,
+    relu_sum8): exact up to the verified step 1024, and >= 1024 wherever the true element is (the
+    window then saturates), for every reachable x."""
+    emax, vmax = 1024, 16 * A + 777
+    rc, mbits, r, c = _floor_form(fac, emax, vmax)
+    assert rc == 0
+    M = int(np.array([mbits], dtype=np.int32).view(np.float32)[0])
+    x = np.arange(-vmax, vmax + 1, dtype=np.int64)
+    g = ((M + x).astype(np.longdouble) * np.longdouble(r) + np.longdouble(c)).astype(np.float32)
+    e = np.maximum(g.view(np.uint32).astype(np.int64) - int(np.array([K]).view(np.uint32)[0]), 0)
+    q = np.sign(x) * np.sign(fac) * (np.abs(x) // abs(fac))
+    want = np.maximum(q, 0)
+    small = want <= emax
+    assert np.array_equal(e[small], want[small]), fac
+    assert (e[~small] >= emax).all(), fac
+
+
 @pytest.mark.parametrize("fac", [(1 << 20) + 7, -(1 << 21) - 1, 2**31 - 1])
 def test_large_factors_at_step_boundaries(fac):
     """|fac| > 2^17: exact fractions at both ends of every step interval (the form is monotone)."""
