@@ -19,7 +19,7 @@ def test_fixtures_regenerate_identical(tmp_path):
     mf.main(str(tmp_path))
     committed = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "fixture_*.npz")))
     made = sorted(os.path.basename(p) for p in glob.glob(os.path.join(str(tmp_path), "fixture_*.npz")))
-    assert committed == made and len(made) == 6
+    assert committed == made and len(made) == 8
     for name in made:
         with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as a, \
                 np.load(os.path.join(str(tmp_path), name), allow_pickle=False) as b:
