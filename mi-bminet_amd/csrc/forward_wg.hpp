@@ -30,10 +30,14 @@
 //                                                    (reference: layer4.c:51-149)
 //   layer5  F2*T64 -> 4 linear + bias + requant: one wave, 16 lanes per class, DPP row
 //           reduction, one dword store.              (reference: layer5.c:43-89)
-// The plain (non-REORDER_BN) build requantises every layer-2/4 element in the floor form (l2n_out).
+// The plain (non-REORDER_BN) build requantises every layer-2/4 element in the floor form (l2n_out,
+// relu_sum8); its 22-channel time-major layer-1 blocks past the VGPR prefetch arrive a trial ahead
+// in LDS by LDS-DMA (Cfg::LDMA).  Parameter sets outside the float requant envelope run Cfg::XR,
+// exact integer division (xdiv) at layers 1, 2 and 4.
 // Channel-major input (Cfg::CT, net_model_compute_batch_ct): each layer-1 block is read as
-// 16-sample row segments, transposed through a per-wave LDS staging area (stage_block) and read
-// back as the MFMA A fragment; everything after that is the same code.
+// 16-sample row segments and transposed through LDS (22 channels: an LDS-DMA ring read back with
+// ds_read_b64_tr_b16; 64 channels: whole rows exchanged through a shared phase image) into the
+// MFMA A fragment; everything after that is the same code.
 #pragma once
 #include "forward_common.hpp"
 #ifdef MIB_DIAG
