@@ -154,15 +154,15 @@ struct Cfg {
   // batched trial stride (bytes): time-major trials are padded to 16 bytes, channel-major ones
   // are the caller's contiguous [B][C][T]
   static constexpr int XTRIAL = FQ ? 4 * C * T : CT ? C * T : align16(T * C);
-  // Channel-major int8, 64 channels, canonical BN (RX): whole-row loads.  Wave w loads channel rows
+  // Channel-major int8, 64 channels, either BN branch (RX): whole-row loads.  Wave w loads channel rows
   // w + 8 h + 16 m (h < 2, m < 4) in 512-byte phases (2 rows x 512 bytes per load, lane-contiguous,
   // where single-block loads read 16 bytes from each of 64 rows), and the waves exchange them
   // through a 32 KB LDS image of one phase: [64 rows][512 bytes], read back with ds_read_b64_tr_b8
   // (rx_*, layer1).  Phase 0 of the next trial is stored before barrier B; each further phase
-  // costs two barriers (the image consumed, the image complete).  Config C -19.6 %.
-  // The other 64-channel builds (plain BN, float input) stage one block at a time (stage_block),
-  // double-buffered in two 1 KB areas per wave.
-  static constexpr bool RX = CT_ && !FQ_ && P == 1 && RB_ && C == 64 && SPL.cl == 0 && (C * T) % 4 == 0;
+  // costs two barriers (the image consumed, the image complete).  Config C -19.6 %;
+  // the plain-BN build since round 5: C -23.0 %, 64x480 -11.0 %.  The float-input 64-channel build
+  // stages one block at a time (stage_block), double-buffered in two 1 KB areas per wave.
+  static constexpr bool RX = CT_ && !FQ_ && P == 1 && C == 64 && SPL.cl == 0 && (C * T) % 4 == 0;
   static constexpr int NPH = RX ? (16 * NB1 + 511) / 512 : 0;  // image phases of 512 samples
   static constexpr int STG = RX ? 32768 / NWAVES : 2048;  // staging bytes per wave
   static constexpr int NB3 = (T8 + 15) / 16;            // layer-3 column blocks of 16 outputs
@@ -1190,6 +1190,12 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
         w = (unsigned)(xelem_sum8<0, 127>(acc, m, R.xs2[fi]) >> 3) | ((unsigned)(xelem_sum8<8, 127>(acc, m, R.xs2[fi]) >> 3) << 8);
       } else {
         w = l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
+        // 64-channel row exchange: both windows are summed on every path (sunk into the last
+        // tile's byte-store branch, the second window's sum left accumulator registers unread on
+        // the other path while the MFMA still wrote them, and the next layer 1's inline-asm pack
+        // reused one: tools/mfma_lint.py, write-after-write; as in layer 4).  Not in the other
+        // builds, where the lint finds no such reuse and the pinned order costs 4.4 % (config B).
+        if constexpr (K::RX) asm volatile("" ::"v"(w));
       }
       int8_t* dst = smem_y2 + f * K::Y2ROW + 128 * mt + T.l2y;
       if (128 * (mt + 1) <= K::T8) {
