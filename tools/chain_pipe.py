@@ -25,9 +25,11 @@ def main():
     ap.add_argument("--chunks", default="2048,4096,8192,16384")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--nbuf", type=int, default=2)
+    ap.add_argument("--cfg", default="b22", choices=("b22", "c64", "p64"))
     a = ap.parse_args()
-    C, T, B = 22, 1125, a.B
-    lib.params_load(ParamSet.synthetic(seed=1))
+    C, T = {"b22": (22, 1125), "c64": (64, 1000), "p64": (64, 480)}[a.cfg]
+    B = a.B
+    lib.params_load(ParamSet.synthetic(seed=1, C=C, T=T))
     stride = lib.trial_stride()
     L = lib.load()
     dev = torch.device("cuda", 0)
@@ -60,6 +62,16 @@ def main():
     torch.cuda.synchronize()
     want = cls.clone()
     print(f"serial: {timed(serial):.3f} ms per {B} trials", flush=True)
+
+    def fused():  # the float entry: quantised inside the forward kernel
+        L.net_model_compute_batch_f32(xf.data_ptr(), logits.data_ptr(), B, scale, 0, s0.cuda_stream)
+        L.net_argmax_batch(logits.data_ptr(), cls.data_ptr(), B, 4, 0, s0.cuda_stream)
+
+    cls.zero_()
+    fused()
+    torch.cuda.synchronize()
+    print(f"fused float entry: {timed(fused):.3f} ms per {B} trials, same classes: {bool(torch.equal(cls, want))}",
+          flush=True)
     sq, sf = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     for K in [int(k) for k in a.chunks.split(",")]:
         bufs = [torch.empty((K, stride), dtype=torch.int8, device=dev) for _ in range(a.nbuf)]
