@@ -1447,7 +1447,8 @@ __global__ __launch_bounds__(NTHREADS) __attribute__((amdgpu_waves_per_eu(WPE, W
     }
   }
   // the last fill (of an empty view past the batch) writes LDS: it lands before the wave ends
-  if constexpr (K::DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // (the channel-major ring and the plain / exact-division LDMA slots alike)
+  if constexpr (K::DMA || K::LDMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   MIB_STAMP_FLUSH(lane == 0, wave)
   MIB_CLOCK_FLUSH
 }

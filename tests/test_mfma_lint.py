@@ -196,7 +196,8 @@ def test_dma_ring_wait_counts_issued_ops(device_asm):
             elif in_asm and i > head and l.startswith("s_waitcnt vmcnt("):
                 waits.append(int(l.split("(")[1].split(")")[0]))
         kind = _dma_kind(name)
-        assert sorted(set(waits)) == ([0, 1] if kind == "ring" else [3]), (name, kind, waits)
+        # (vmcnt(0) after the loop: the last fill lands before the wave ends)
+        assert sorted(set(waits)) == ([0, 1] if kind == "ring" else [0, 3]), (name, kind, waits)
         after = [l for l in lines[loop_fills[-1] + 1:]
                  if l.startswith(("global_store", "buffer_store", "global_load", "buffer_load")) and not l.endswith(" lds")]
         if kind == "ring":
