@@ -40,7 +40,8 @@ extern "C" {
 #define NET_OK 0
 #define NET_ERR_INVALID (-1)     /* bad argument (null pointer, bad size, bad device) */
 #define NET_ERR_NO_PARAMS (-2)   /* no parameter blob loaded */
-#define NET_ERR_UNSUPPORTED (-3) /* network dimensions without a compiled gfx950 kernel */
+#define NET_ERR_UNSUPPORTED (-3) /* network dimensions outside what the kernels take: F1 = F2 = 16, D = 1,
+                                    C <= 64, 64 <= T <= 4096, N <= 16 */
 #define NET_ERR_BLOB (-4)        /* malformed parameter blob */
 #define NET_ERR_RANGE (-5)       /* parameters on which the reference's int32 arithmetic is undefined
                                     (overflow, zero divisor), or a float-input scale outside
@@ -80,7 +81,11 @@ int net_last_error(void);
  * BN branches of layer2.c:139-210 / layer4.c:91-133.  Flag bit 1: clip every requantised output to
  * [-127, 127], the golden model's clip_balanced=True, functional.py:89-91; clear: [-128, 127] as
  * the C's __CLIP_R).  Other flag bits are rejected (NET_ERR_BLOB).  Validates, precomputes the gfx950 operand fragments and exact requantisation
- * constants, and uploads lazily to each device on first use.  Every set on which the reference's
+ * constants, and uploads lazily to each device on first use.  Geometry: F1 = F2 = 16 and D = 1
+ * (layer2.c:246), any C <= 64, 64 <= T <= 4096 and 1 <= N <= 16 (the channel-selected and 2- or
+ * 3-class networks of QuantLab's loaders included); 22 x 1125, 64 x 1000 and 64 x 480 with N = 4
+ * run kernels compiled for those shapes, every other geometry the run-time-dimension kernels
+ * (net_params_info reports which).  Every set on which the reference's
  * own int32 arithmetic is defined for every int8 input loads: sets inside the float requant
  * envelope run the float-requant kernels, the others (e.g. large folded BN offsets) kernels that
  * divide exactly in integers.  NET_ERR_RANGE only where the reference's arithmetic is undefined:
@@ -89,19 +94,35 @@ int net_last_error(void);
  * layer4.c:99-130), or of the plain layer 4's sum of eight elements (layer4.c:113-130).  Replaces any previous set.  Pad
  * bytes of net_l1_weight_align (channels C..C_ALIGN-1) and of net_l5_weight (columns
  * T64..T64_ALIGN-1 of every row) must be zero, as gen_net_header.py writes them (NET_ERR_BLOB
- * otherwise).  Each distinct set gets its own device copy (about 72 KB per set and device), which
+ * otherwise).  Each distinct set gets its own device copy (about 144 KB per set and device), which
  * is never overwritten: launches already enqueued, and launches captured into a HIP graph, keep
- * running the set (and build variant) they were enqueued with, whatever is loaded later.  At most
- * 8 copies are kept per device: uploading a ninth synchronises the device and frees the least
- * recently used ones, so a HIP graph that captured a launch with an evicted set must be
- * re-captured. */
+ * running the set (and build variant) they were enqueued with, whatever is loaded later.  A load
+ * never waits for the device.  When a device already holds 8 copies, the least recently used
+ * copies whose launches have all completed are freed first (a copy is freed only once no launch
+ * can still read it); if none is idle, the device keeps more than 8.  A copy used by a launch
+ * under stream capture (which a HIP graph may replay at any time) is pinned until
+ * net_params_unload, so captured graphs stay valid across any number of later loads.  A set
+ * loaded again reuses its copy. */
 int net_params_load(const void* blob, size_t len);
+
+/* Which kernels the loaded set runs, for integrators who need to see a slower path coming:
+ * info[0] = NET_PATH_FLOAT (compiled geometry, float requant proven exact on every reachable
+ * value), NET_PATH_EXACT (compiled geometry, exact integer division at layers 1, 2 and 4: about
+ * 1.5x the float kernels' time on 22 x 1125) or NET_PATH_GENERAL (run-time-dimension kernels,
+ * exact division throughout); info[1] = the layer (1, 2 or 4) of the first requant that has no
+ * proven float form (NET_PATH_EXACT), else 0; info[2] = its filter, else -1; info[3] = the
+ * compiled geometry (0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480), -1 on the general path. */
+#define NET_PATH_FLOAT 0
+#define NET_PATH_EXACT 1
+#define NET_PATH_GENERAL 2
+int net_params_info(int32_t* info);
 
 /* dims[0..6] = C, T, F1, F2, N, weight_bits, loaded(0/1). */
 int net_params_dims(int32_t* dims);
 
 /* Drops the loaded set and frees every device copy of every set, after synchronising each device
- * that holds copies (HIP graphs capturing launches must be dropped first). */
+ * that holds copies (HIP graphs capturing launches must be dropped first: this is the one call
+ * after which a captured launch may no longer be replayed). */
 void net_params_unload(void);
 
 /* ---- batched device entry points ---------------------------------------------------------- */

@@ -65,6 +65,11 @@ int mibminet_test_pool_consts(int32_t off, int32_t layer, int32_t* thr, int32_t*
  * kernels, NET_ERR_NO_PARAMS when none is loaded. */
 int mibminet_test_params_xr(void);
 
+/* on != 0: every parameter set loaded after this call runs the run-time-dimension kernels
+ * (forward_gen.hpp), the compiled geometries included, so that both kernel families can be
+ * checked against the oracle on the same set; 0 restores the normal choice. */
+int mibminet_test_force_general(int on);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,456 @@
+// forward_gen.hpp — gfx950 fused forward for every network geometry the reference's generator
+// emits (edge-eegnet_wolf/data/gen_net_header.py:78-89): C <= 64 channels (channel-selected
+// MI-BMInet inputs, QuantLab/.../PhysionetMMMI/edgeEEGNet/preprocess.py:86-87), 64 <= T <= 4096
+// samples (every time window of the loaders: 480 and 960 in get_data.py:156-159, 1125 for
+// BCI-IV-2a), 1 <= N <= 16 classes (the 2- and 3-class PhysioNet nets, get_data.py:73-82), with
+// F1 = F2 = 16 and D = 1 as layer2.c:246 fixes them.
+//
+// The dimensions are kernel-uniform run-time values (GenParams), so one compiled kernel per input
+// layout serves every geometry; the three geometries of the reference's own configurations keep
+// their compile-time specialisations (forward_wg.hpp), which this file does not touch.
+//
+// One workgroup of NW = 8 wave64s owns one trial at a time (persistent, grid-strided), with three
+// barriers per trial.  Every intermediate stays in LDS:
+//   layer1  MFMA i32_16x16x64_i8: A = 16 samples x 64 channel slots, B = the 16 filters' weights
+//           (zero past C), C-init = the offset.  Time-major trials: a lane's 16 bytes of sample
+//           t are t C + 16 g .. +15 of the trial, read as five aligned dwords and realigned by
+//           v_alignbyte (no load straddles the view, so no byte is lost to the per-dword range
+//           check); channel-major trials (int8 or float32, quantised here) go through the same
+//           LDS transpose as the specialised kernels (wg::stage_block, ds_read_b64_tr_b8).
+//                                                               (reference: layer1.c:53-101)
+//   layer2  the 64-tap depthwise xcorr as a banded-Toeplitz GEMM on MFMA i32_32x32x32_i8 (A = 32
+//           output shifts x 96-tap band, rows permuted so that a lane holds two whole pool-8
+//           windows; B = 16-byte slices of the layer-1 row), ReLU-pool and requant per lane.
+//                                                               (reference: layer2.c:56-118, 139-210)
+//   layer3  16-tap depthwise conv on the VALU: four outputs per lane from five aligned dwords of
+//           the layer-2 row against four pre-shifted tap vectors (v_dot4_i32_i8), written
+//           transposed [u][f] (the reference's flip is index math).   (reference: layer3.c:49-79)
+//   layer4  16x16 pointwise on the VALU (v_dot4), ReLU-pool and requant.  (reference: layer4.c:51-149)
+//   layer5  N-class linear layer: one wave per class, v_dot4 + a wave reduction.  (reference: layer5.c:43-89)
+// Every requantisation is exact integer division (xdiv, forward_common.hpp), so every parameter
+// set the reference's int32 arithmetic defines runs here without a float envelope.
+#pragma once
+#include "forward_wg.hpp"
+
+namespace mib {
+namespace gen {
+
+constexpr int NW = 8;                  // waves per workgroup
+constexpr int NT = 64 * NW;
+constexpr int TMAX = 4096;             // samples per trial (16 s at 250 Hz)
+constexpr int NMAX = 16;               // classes
+constexpr int T64A_MAX = TMAX / 64;
+constexpr int L5W = F2 * T64A_MAX;     // bytes of one class's layer-5 weight row
+
+enum Layout { TM = 0, CT = 1, F32 = 2 };
+
+// Per-filter constants read by layers 3 and 4 of every wave: copied into LDS once per workgroup.
+struct SmallG {
+  int l3_w[F2][4][8];     // layer 3: output phase k = u & 3: byte q < 20 of the 20-byte window at
+                          // u & ~3 meets tap W3t[q - k - 1] (dwords 0..4; 5..7 zero)
+  int l4_w[F2][4];        // layer 4: weight row k, 16 bytes
+  int l4_thr[F2];         // REORDER_BN: -(offset >> 3); plain: unused
+  int l4_off[F2];         // REORDER_BN: offset; plain: offset >> 3
+  unsigned l4_m[F2];      // xdiv magic of factor (plain: factor >> 3)
+  int l4_xs[F2];
+};
+static_assert(sizeof(SmallG) % 16 == 0, "SmallG is copied in 16-byte pieces");
+
+// Device parameter image of the general path (built on the host: mibminet.hip, build_genparams).
+struct GenParams {
+  int C, T, N, T8;
+  int T64, T64A, NB1, MT;       // NB1: layer-1 blocks of 16 samples; MT: layer-2 tiles of 1024 outputs
+  int rb, lo, xstride, pad0;    // REORDER_BN branches; lower clip bound; time-major trial stride
+  unsigned l3_m;
+  int l3_xs;
+  unsigned l5_m;
+  int l5_xs;
+  v4i l1_b[64];                 // layer-1 B operand: lane (filter lane & 15, g) = W1[f][16 g .. +15]
+  int l1_off[F2];
+  unsigned l1_m[F2];
+  int l1_xs[F2];
+  int l2_thr[F2];               // REORDER_BN: -(offset >> 3); plain: unused
+  int l2_off[F2];               // REORDER_BN: offset; plain: offset >> 3
+  unsigned l2_m[F2];            // xdiv magic of factor (plain: factor >> 3)
+  int l2_xs[F2];
+  int l5_b[NMAX];
+  SmallG sg;
+  v4i l2_a[F2][3][64];          // layer-2 A operand (banded weights) per filter, K-step and lane
+  int8_t l5_w[NMAX][L5W];       // [n][k T64A + v], zero pads
+};
+
+// LDS carve of one workgroup (host and device compute it alike).
+struct Carve {
+  int y1s, y2s;                 // row strides of y1 (positions t + 32) and y2 (positions u + 8)
+  int y2, y3, y4, sg, stg, bytes;
+};
+__host__ __device__ inline Carve carve_of(int T8, int T64A, int NB1, int MT, bool staging) {
+  Carve c;
+  // layer 2 reads positions < 1024 MT + 64; layer 1 writes positions < 32 + 16 NB1.  Stride = 16
+  // (mod 256): the sixteen filters' layer-1 dword stores of a block fall on distinct banks
+  const int need = cmax(32 + 16 * NB1, 1024 * MT + 64);
+  c.y1s = (need + 239) / 256 * 256 + 16;
+  c.y2s = align16(T8 + 32);     // 8 pad bytes, T8 outputs, zeros under layer 3's 20-byte windows
+  c.y2 = 16 * c.y1s;
+  c.y3 = c.y2 + 16 * c.y2s;
+  c.y4 = c.y3 + align16(16 * T8);
+  c.sg = c.y4 + align16(16 * T64A);
+  c.stg = c.sg + (int)sizeof(SmallG);
+  c.bytes = c.stg + (staging ? NW * 1024 : 0);
+  return c;
+}
+
+__device__ __forceinline__ int clampq(int v, int lo) { return min(max(v, lo), 127); }
+__device__ __forceinline__ unsigned pack4(int a, int b, int c, int d) {
+  return (unsigned)(a & 255) | ((unsigned)(b & 255) << 8) | ((unsigned)(c & 255) << 16) | ((unsigned)d << 24);
+}
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// 16 bytes at byte offset o of the view, from five aligned dwords: each dword lies wholly inside
+// or wholly outside num_records (which is a multiple of 4), so the range check zeroes no byte the
+// trial holds.  v_alignbyte_b32(hi, lo, s) = bytes s .. s + 3 of hi:lo.
+__device__ __forceinline__ v4i load16u(wg::Rsrc r, int o) {
+  const int o4 = o & ~3;
+  const unsigned s = (unsigned)(o & 3);
+  const v4u a = __builtin_amdgcn_raw_buffer_load_b128(r, o4, 0, 0);
+  const unsigned e = __builtin_amdgcn_raw_buffer_load_b32(r, o4 + 16, 0, 0);
+  return (v4i){(int)__builtin_amdgcn_alignbyte(a[1], a[0], s), (int)__builtin_amdgcn_alignbyte(a[2], a[1], s),
+               (int)__builtin_amdgcn_alignbyte(a[3], a[2], s), (int)__builtin_amdgcn_alignbyte(e, a[3], s)};
+}
+
+// The view of trial b: base = the trial's first byte rounded down to a dword, delta = the rest,
+// num_records = the trial's bytes from base rounded up to a dword (a dword holding a trial byte is
+// inside the page of that byte, so the rounding reads no unmapped memory).
+struct View {
+  wg::Rsrc r;
+  int delta;
+};
+template <int L>
+__device__ __forceinline__ View trial_view(const int8_t* x, long long b, int C, int T, int xstride) {
+  const long long ct = (long long)C * T;
+  const int8_t* p = L == TM ? x + b * xstride : L == CT ? x + b * ct : x + 4 * b * ct;
+  const int delta = (int)((size_t)p & 3);
+  const int bytes = (int)((L == F32 ? 4 : 1) * ct);
+  View v;
+  v.r = __builtin_amdgcn_make_buffer_rsrc((void*)(p - delta), (short)0, (delta + bytes + 3) & ~3, 0x00020000);
+  v.delta = delta;
+  return v;
+}
+
+// The A fragment of layer-1 block blk (samples 16 blk .. +15), before staging: time-major, lane
+// (j, g) holds channels 16 g .. +15 of sample 16 blk + j (bytes past the sample's C meet zero
+// weights); channel-major, lane c holds samples 16 blk .. +15 of channel c (0 for c >= C).
+template <int L>
+__device__ __forceinline__ v4i l1_fetch(const View& v, int blk, int C, int T, int lane, float qs, float qy) {
+  if constexpr (L == TM) {
+    const int j = lane & 15, g = lane >> 4;
+    if (16 * g >= C) return (v4i){0, 0, 0, 0};
+    return load16u(v.r, v.delta + (16 * blk + j) * C + 16 * g);
+  } else if constexpr (L == CT) {
+    if (lane >= C) return (v4i){0, 0, 0, 0};
+    return load16u(v.r, v.delta + lane * T + 16 * blk);
+  } else {
+    if (lane >= C) return (v4i){0, 0, 0, 0};
+    v4i w;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const v4u f = __builtin_amdgcn_raw_buffer_load_b128(v.r, 4 * (lane * T + 16 * blk) + 16 * m, 0, 0);
+      // the reference's input quantisation (gen_input_header.py:66-76), wg::quantize1_f; the
+      // truncating convert lies in [-127, 127]
+      int q[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) q[i] = (int)wg::quantize1_f(__uint_as_float(f[i]), qs, qy);
+      w[m] = (int)pack4(q[0], q[1], q[2], q[3]);
+    }
+    return w;
+  }
+}
+
+struct TrK {
+  static constexpr bool TR16 = false;  // wg::stage_block's P == 1 transpose (ds_read_b64_tr_b8)
+};
+
+// Layer 1: this wave's blocks blk = wave, wave + NW, ... -> y1 rows (position 32 + t).  Loads of
+// U blocks are issued before their MFMAs.
+template <int L>
+__device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const View& v, int8_t* y1, int y1s,
+                                       int8_t* stg, const v4i& wf, int off, unsigned m, int xs, int wave, int lane,
+                                       float qs, float qy) {
+  const int C = gp->C, T = gp->T, NB1 = gp->NB1, lo = gp->lo;
+  const int j = lane & 15, g = lane >> 4;
+  constexpr int U = L == F32 ? 2 : 4;
+  for (int b0 = wave; b0 < NB1; b0 += U * NW) {
+    v4i raw[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int blk = b0 + u * NW;
+      raw[u] = blk < NB1 ? l1_fetch<L>(v, blk, C, T, lane, qs, qy) : (v4i){0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int blk = b0 + u * NW;
+      if (blk < NB1) {  // wave-uniform
+        const v4i a = L == TM ? raw[u] : wg::stage_block<TrK>(raw[u], stg, lane);
+        const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wf, (v4i){off, off, off, off}, 0, 0, 0);
+        // lane column j = filter j, rows 4 g + r = samples 16 blk + 4 g + r
+        const int t0 = 16 * blk + 4 * g;
+        int y[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) y[r] = t0 + r < T ? clampq(xdiv(acc[r], m, xs), lo) : 0;
+        *(unsigned*)(y1 + j * y1s + 32 + t0) = pack4(y[0], y[1], y[2], y[3]);
+      }
+    }
+  }
+}
+
+// Layer 2 (layer2.c:56-118 REORDER_BN, :139-210 plain): the wave's filters 2 wave + fi.  Lane
+// (n, h) of tile mt holds conv outputs 1024 mt + 32 n + 16 h + r (r < 16), i.e. the pool windows
+// u0 = 128 mt + 4 n + 2 h and u0 + 1.
+__device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const int8_t* y1, int y1s, int8_t* y2, int y2s,
+                                       const v4i (&af)[2][3], const int (&thr)[2], const int (&off)[2],
+                                       const unsigned (&m)[2], const int (&xs)[2], int wave, int lane) {
+  const int T8 = gp->T8, MT = gp->MT, lo = gp->lo;
+  const bool rb = gp->rb != 0;
+  const int n = lane & 31, h = lane >> 5;
+  for (int mt = 0; mt < MT; mt++) {
+#pragma unroll
+    for (int fi = 0; fi < 2; fi++) {
+      const int f = 2 * wave + fi;
+      const int8_t* pb = y1 + f * y1s + 1024 * mt + 32 * n + 16 * h;
+      v16i acc;
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[i] = 0;
+#pragma unroll
+      for (int s = 0; s < 3; s++)
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[fi][s], *(const v4i*)(pb + 32 * s), acc, 0, 0, 0);
+      int q[2];
+#pragma unroll
+      for (int w = 0; w < 2; w++) {
+        int sum = 0;
+        if (rb) {
+#pragma unroll
+          for (int i = 0; i < 8; i++) sum += max(acc[8 * w + i], thr[fi]);
+          q[w] = clampq(xdiv(sum + off[fi], m[fi], xs[fi]), lo);
+        } else {
+          // func_xcorr_scale per element (clip to int8), ReLU, sum of 8 >> 3
+#pragma unroll
+          for (int i = 0; i < 8; i++) sum += min(max(xdiv(acc[8 * w + i] + off[fi], m[fi], xs[fi]), 0), 127);
+          q[w] = clampq(sum >> 3, lo);
+        }
+      }
+      const int u0 = 128 * mt + 4 * n + 2 * h;
+      int8_t* dst = y2 + f * y2s + 8 + u0;
+      if (u0 + 1 < T8) *(unsigned short*)dst = (unsigned short)((q[0] & 255) | ((q[1] & 255) << 8));
+      else if (u0 < T8) *dst = (int8_t)q[0];
+    }
+  }
+}
+
+// Layer 3 (layer3.c:49-79, conv.c:105): output u of filter f = sum_j y2p[u + j] W3t[j], y2p[i] at
+// row byte i + 1; four outputs u0 .. u0 + 3 per item from row bytes u0 .. u0 + 19.  Written to
+// y3t[u][f] (net_layer3_flip_inplace as index math).
+__device__ __forceinline__ void layer3(const GenParams* __restrict__ gp, const int8_t* y2, int y2s, int8_t* y3,
+                                       const SmallG* sg, int wave, int lane) {
+  const int T8 = gp->T8, lo = gp->lo;
+  const unsigned m = gp->l3_m;
+  const int xs = gp->l3_xs;
+  const int G = (T8 + 3) >> 2;
+  for (int it = lane; it < 2 * G; it += 64) {
+    const int fi = it >= G, u0 = 4 * (it - fi * G), f = 2 * wave + fi;
+    const int* row = (const int*)(y2 + f * y2s + u0);
+    int d[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) d[i] = row[i];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      int acc = 0;
+#pragma unroll
+      for (int i = 0; i < 5; i++) acc = __builtin_amdgcn_sdot4(d[i], sg->l3_w[f][k][i], acc, false);
+      if (u0 + k < T8) y3[16 * (u0 + k) + f] = (int8_t)clampq(xdiv(acc, m, xs), lo);
+    }
+  }
+}
+
+// Layer 4 (layer4.c:51-149, FLIP_LAYERS): item (k, v): b = W4[k] . y3t[u] for u = 8 v .. 8 v + 7,
+// REORDER_BN: sum max(b, thr) + off, / fac; plain: sum max(tdiv(b + off >> 3, fac >> 3), 0) >> 3.
+__device__ __forceinline__ void layer4(const GenParams* __restrict__ gp, const int8_t* y3, int8_t* y4,
+                                       const SmallG* sg, int tid) {
+  const int T64 = gp->T64, T64A = gp->T64A, lo = gp->lo;
+  const bool rb = gp->rb != 0;
+  for (int it = tid; it < F2 * T64; it += NT) {
+    const int k = it & 15, v = it >> 4;
+    const v4i w = *(const v4i*)sg->l4_w[k];
+    const int thr = sg->l4_thr[k], off = sg->l4_off[k], xs = sg->l4_xs[k];
+    const unsigned m = sg->l4_m[k];
+    int sum = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const v4i a = *(const v4i*)(y3 + 16 * (8 * v + i));
+      int b = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) b = __builtin_amdgcn_sdot4(a[q], w[q], b, false);
+      sum += rb ? max(b, thr) : max(xdiv(b + off, m, xs), 0);
+    }
+    y4[k * T64A + v] = (int8_t)clampq(rb ? xdiv(sum + off, m, xs) : sum >> 3, lo);
+  }
+}
+
+// Layer 5 (layer5.c:43-89, transform.c:47): class n on wave n mod NW; z = W5[n] . y4 + b5[n],
+// clip(z / fac) (pad columns meet zero weights).
+__device__ __forceinline__ void layer5(const GenParams* __restrict__ gp, const int8_t* y4, int8_t* out, int wave,
+                                       int lane) {
+  const int N = gp->N, nd = 4 * gp->T64A, lo = gp->lo;  // dwords of y4
+  for (int n = wave; n < N; n += NW) {
+    const int* w = (const int*)gp->l5_w[n];
+    int part = 0;
+    for (int d = lane; d < nd; d += 64) part = __builtin_amdgcn_sdot4(((const int*)y4)[d], w[d], part, false);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (lane == 0) out[n] = (int8_t)clampq(xdiv(part + gp->l5_b[n], gp->l5_m, gp->l5_xs), lo);
+  }
+}
+
+// Per-lane constants and the LDS initialisation shared by both kernels.
+struct Lane {
+  v4i wf;             // layer-1 B operand
+  int off1, xs1;
+  unsigned m1;
+  v4i af[2][3];       // layer-2 bands of the wave's two filters
+  int thr2[2], off2[2], xs2[2];
+  unsigned m2[2];
+};
+
+__device__ __forceinline__ void setup(const GenParams* __restrict__ gp, int8_t* smem, const Carve& cv, Lane& R,
+                                      int tid, int wave, int lane) {
+  const int j = lane & 15;
+  R.wf = gp->l1_b[lane];
+  R.off1 = gp->l1_off[j];
+  R.m1 = gp->l1_m[j];
+  R.xs1 = gp->l1_xs[j];
+#pragma unroll
+  for (int fi = 0; fi < 2; fi++) {
+    const int f = 2 * wave + fi;
+#pragma unroll
+    for (int s = 0; s < 3; s++) R.af[fi][s] = gp->l2_a[f][s][lane];
+    R.thr2[fi] = gp->l2_thr[f];
+    R.off2[fi] = gp->l2_off[f];
+    R.m2[fi] = gp->l2_m[f];
+    R.xs2[fi] = gp->l2_xs[f];
+  }
+  // zero pads of every row (positions past the data are never rewritten), then the small params
+  v4i* z = (v4i*)smem;
+  for (int i = tid; i < cv.sg / 16; i += NT) z[i] = (v4i){0, 0, 0, 0};
+  const v4i* src = (const v4i*)&gp->sg;
+  v4i* dst = (v4i*)(smem + cv.sg);
+  for (int i = tid; i < (int)(sizeof(SmallG) / 16); i += NT) dst[i] = src[i];
+}
+
+// Fused forward over a batch of B trials (layout L), logits [B][N].
+template <int L>
+__global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp, const int8_t* __restrict__ x,
+                                                 int8_t* __restrict__ out, int B, float qs, float qy) {
+  extern __shared__ v4i smem_v[];
+  int8_t* smem = (int8_t*)smem_v;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Carve cv = carve_of(gp->T8, gp->T64A, gp->NB1, gp->MT, L != TM);
+  Lane R;
+  setup(gp, smem, cv, R, tid, wave, lane);
+  const SmallG* sg = (const SmallG*)(smem + cv.sg);
+  int8_t* y1 = smem;
+  int8_t* y2 = smem + cv.y2;
+  int8_t* y3 = smem + cv.y3;
+  int8_t* y4 = smem + cv.y4;
+  int8_t* stg = smem + cv.stg + 1024 * wave;
+  const int C = gp->C, T = gp->T, N = gp->N, xstride = gp->xstride;
+  __syncthreads();
+  // Barriers per trial: A (layer 2 reads every wave's layer-1 rows), B (layer 4 reads every
+  // filter), C (layer 5 reads all of y4).  The next trial's layer 1 writes only y1, last read
+  // before B; its layers 2-3 come after the next A, which every wave reaches only after C.
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    const View v = trial_view<L>(x, b, C, T, xstride);
+    layer1<L>(gp, v, y1, cv.y1s, stg, R.wf, R.off1, R.m1, R.xs1, wave, lane, qs, qy);
+    __syncthreads();  // A
+    layer2(gp, y1, cv.y1s, y2, cv.y2s, R.af, R.thr2, R.off2, R.m2, R.xs2, wave, lane);
+    wg::wave_sync_lds();  // layer 3 of filter f reads only y2 row f, written by this wave
+    layer3(gp, y2, cv.y2s, y3, sg, wave, lane);
+    __syncthreads();  // B
+    layer4(gp, y3, y4, sg, tid);
+    __syncthreads();  // C
+    layer5(gp, y4, out + (size_t)b * N, wave, lane);
+  }
+}
+
+// Single-trial, single-layer kernel for the reference's per-layer entry points on the general
+// path: stage 1..5 = net_layerN, 6 = net_layer3_flip_inplace; reference layouts in and out (pads
+// zero).  Stage 1 takes the trial packed time-major [T][C] (the batched layout).
+__global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, const int8_t* __restrict__ in,
+                                              int8_t* __restrict__ out, int stage) {
+  extern __shared__ v4i smem_v[];
+  int8_t* smem = (int8_t*)smem_v;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const Carve cv = carve_of(gp->T8, gp->T64A, gp->NB1, gp->MT, false);
+  Lane R;
+  setup(gp, smem, cv, R, tid, wave, lane);
+  const SmallG* sg = (const SmallG*)(smem + cv.sg);
+  int8_t* y1 = smem;
+  int8_t* y2 = smem + cv.y2;
+  int8_t* y3 = smem + cv.y3;
+  int8_t* y4 = smem + cv.y4;
+  const int C = gp->C, T = gp->T, T8 = gp->T8, T64 = gp->T64, T64A = gp->T64A;
+  const int TA = (T + 3) & ~3, T8A = (T8 + 3) & ~3;
+  __syncthreads();
+  if (stage == 1) {  // [T][C] packed -> [F1][T_ALIGN]
+    const View v = trial_view<TM>(in, 0, C, T, gp->xstride);
+    layer1<TM>(gp, v, y1, cv.y1s, nullptr, R.wf, R.off1, R.m1, R.xs1, wave, lane, 0.0f, 0.0f);
+    __syncthreads();
+    for (int i = tid; i < F2 * TA; i += NT) {
+      const int f = i / TA, t = i - f * TA;
+      out[i] = t < T ? y1[f * cv.y1s + 32 + t] : 0;
+    }
+  } else if (stage == 2) {  // [F1][T_ALIGN] -> [F2][T8_ALIGN]
+    for (int i = tid; i < F2 * T; i += NT) {
+      const int f = i / T, t = i - f * T;
+      y1[f * cv.y1s + 32 + t] = in[f * TA + t];
+    }
+    __syncthreads();
+    layer2(gp, y1, cv.y1s, y2, cv.y2s, R.af, R.thr2, R.off2, R.m2, R.xs2, wave, lane);
+    __syncthreads();
+    for (int i = tid; i < F2 * T8A; i += NT) {
+      const int f = i / T8A, u = i - f * T8A;
+      out[i] = u < T8 ? y2[f * cv.y2s + 8 + u] : 0;
+    }
+  } else if (stage == 3) {  // [F2][T8_ALIGN] -> [F2][T8_ALIGN]
+    for (int i = tid; i < F2 * T8; i += NT) {
+      const int f = i / T8, u = i - f * T8;
+      y2[f * cv.y2s + 8 + u] = in[f * T8A + u];
+    }
+    __syncthreads();
+    layer3(gp, y2, cv.y2s, y3, sg, wave, lane);
+    __syncthreads();
+    for (int i = tid; i < F2 * T8A; i += NT) {
+      const int f = i / T8A, u = i - f * T8A;
+      out[i] = u < T8 ? y3[16 * u + f] : 0;
+    }
+  } else if (stage == 4) {  // [T8][F2] -> [F2][T64_ALIGN]
+    for (int i = tid; i < T8 * F2; i += NT) y3[i] = in[i];
+    __syncthreads();
+    layer4(gp, y3, y4, sg, tid);
+    __syncthreads();
+    for (int i = tid; i < F2 * T64A; i += NT) out[i] = y4[i];
+  } else if (stage == 5) {  // [F2][T64_ALIGN] -> [N] (the pad columns read as zero)
+    for (int i = tid; i < F2 * T64A; i += NT) y4[i] = (i % T64A) < T64 ? in[i] : 0;
+    __syncthreads();
+    layer5(gp, y4, out, wave, lane);
+  } else if (stage == 6) {  // flip [F2][T8_ALIGN] -> [T8][F2]
+    for (int i = tid; i < F2 * T8A; i += NT) {
+      const int u = i / F2, f = i - u * F2;
+      out[i] = u < T8 ? in[f * T8A + u] : 0;
+    }
+  }
+}
+
+}  // namespace gen
+}  // namespace mib

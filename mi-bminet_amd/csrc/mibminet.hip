@@ -23,6 +23,7 @@
 #include "../../include/mibminet.h"
 #include "../../include/mibminet_testing.h"
 #include "forward_wg.hpp"
+#include "forward_gen.hpp"
 #include "quantize.hpp"
 #include "classify.hpp"
 
@@ -67,7 +68,12 @@ struct HostParams {
   bool reorder_bn = true;  // blob flag: -DREORDER_BN variant (canonical) or the plain BN branches
   bool clip_balanced = false;  // blob flag: clip to [-127, 127] (golden model's default; the C clips to -128)
   bool xr = false;             // set at load: exact integer division at layers 1, 2, 4 (Cfg::XR)
+  int xr_layer = 0, xr_filter = -1;  // the first requant without a proven float form (xr = true)
+  bool general = false;        // set at load: the run-time-dimension kernels (forward_gen.hpp)
 };
+
+// test hook (mibminet_test_force_general): load every later set on the general path
+std::atomic<int> g_force_general{0};
 
 // ---- exact requantisation ------------------------------------------------------------------
 // y = clip(trunc(v / fac), -128, 127) is computed on the GPU as clip((int)((float)v * r)).
@@ -382,18 +388,19 @@ int parse_blob(const void* blob, size_t len, HostParams& hp) {
 //  * otherwise the exact-division kernels (hp.xr = true, Cfg::XR: xdiv at layers 1, 2 and 4).
 // Layers 3 and 5 always use the float form (|acc| <= 16 * 128^2 and F2 * T64 * 128^2 + 128, every
 // int32 factor proven: tests/test_requant_exact.py).
-int build_devparams(HostParams& hp, DevParams& dp) {
+// Reachable ranges of the layer-1, -2 and -4 requant numerators, and NET_ERR_RANGE where the
+// reference's int32 arithmetic is undefined for some int8 input (both kernel families).
+struct Ranges {
+  Range e1[F2], s2[F2], s4[F2];
+};
+int check_ranges(const HostParams& hp, Ranges& rg) {
   const Dims& d = hp.d;
-  if (d.F1 != F2 || d.F2 != F2 || d.N != N_OUT) return NET_ERR_UNSUPPORTED;
-  if (d.C > 64) return NET_ERR_UNSUPPORTED;
-  const int P = d.C <= 32 ? 2 : 1;
   const int C = d.C, CA = d.C_ALIGN();
-  std::memset(&dp, 0, sizeof(dp));
-  auto w1 = [&](int f, int c) -> int { return hp.l1_weight_align[(size_t)f * CA + c]; };
-  const int64_t A = 128 * 128;
+  Range* e1 = rg.e1;
+  Range* s2 = rg.s2;
+  Range* s4 = rg.s4;
   // reachable ranges: e1 = dot + off1 (layer 1); RB: the pooled sums + offset of layers 2 and 4;
   // plain: the per-element numerators conv + (off >> 3)
-  Range e1[F2], s2[F2], s4[F2];
   for (int f = 0; f < F2; f++) {
     const Range r1 = dot_range(&hp.l1_weight_align[(size_t)f * CA], C);
     const Range r2 = dot_range(&hp.l2_weight_reverse[(size_t)f * 64], 64);
@@ -416,9 +423,54 @@ int build_devparams(HostParams& hp, DevParams& dp) {
     }
   }
   if (hp.l3_factor == 0 || hp.l5_factor == 0) return NET_ERR_RANGE;
+  return NET_OK;
+}
+
+// Layer-2 A operand = banded weights (wg::layer2 and gen::layer2): row i <-> shift n(i) so that
+// lane (c, h) register r holds output shift 16h + r (two complete pool-8 windows per lane).  PL:
+// layer-1 row layout, 2 = parity-split planes (the specialised C <= 32 kernels), 1 = natural order.
+void l2_bands(const HostParams& hp, int PL, v4i (*afrag)[3][64]) {
+  for (int f = 0; f < F2; f++)
+    for (int s = 0; s < 3; s++)
+      for (int lane = 0; lane < 64; lane++) {
+        const int i = lane & 31, hh = lane >> 5;
+        const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
+        int8_t bytes[16];
+        for (int jj = 0; jj < 16; jj++) {
+          const int kq = 32 * s + 16 * hh + jj;  // K-slot
+          // position in the 96-byte row window.  PL == 2: lane half hh reads
+          // parity plane hh, bytes 16s .. 16s+15 of the block's window; PL == 1: natural order.
+          const int kp = PL == 2 ? 2 * (16 * s + jj) + hh : kq;
+          const int idx = kp - n - 1;            // tap (torch order)
+          bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
+        }
+        std::memcpy(&afrag[f][s][lane], bytes, 16);
+      }
+}
+
+int build_devparams(HostParams& hp, DevParams& dp) {
+  const Dims& d = hp.d;
+  if (d.F1 != F2 || d.F2 != F2 || d.N != N_OUT) return NET_ERR_UNSUPPORTED;
+  if (d.C > 64) return NET_ERR_UNSUPPORTED;
+  const int P = d.C <= 32 ? 2 : 1;
+  const int C = d.C, CA = d.C_ALIGN();
+  std::memset(&dp, 0, sizeof(dp));
+  auto w1 = [&](int f, int c) -> int { return hp.l1_weight_align[(size_t)f * CA + c]; };
+  const int64_t A = 128 * 128;
+  Ranges rg;
+  if (const int rc = check_ranges(hp, rg)) return rc;
+  const Range* e1 = rg.e1;
+  const Range* s2 = rg.s2;
+  const Range* s4 = rg.s4;
   // Requant constants of layers 1, 2 and 4.  Float forms (xr = false) fail when a range leaves
   // the float window (|v| < 2^22 for a magic-offset C-init, 2^24 for a converted pooled sum) or a
-  // reciprocal / floor form is not proven; the exact forms (xr = true) always succeed.
+  // reciprocal / floor form is not proven; the exact forms (xr = true) always succeed.  The first
+  // failing requant (layer, filter) is kept for net_params_info.
+  auto fail = [&](int layer, int f) {
+    hp.xr_layer = layer;
+    hp.xr_filter = f;
+    return false;
+  };
   auto requant = [&](bool xr) -> bool {
     SmallParams& sp = dp.sp;
     for (int t = 0; t < P; t++)
@@ -433,7 +485,7 @@ int build_devparams(HostParams& hp, DevParams& dp) {
           dp.l1_cinit[t][j] = hp.l1_offset[f] + FMAGIC_I;
           if (e1[f].amax() >= (1 << 22) ||
               !choose_reciprocal(hp.l1_factor[f], &dp.l1_r[t][j], &dp.l1_c[t][j], 128, e1[f].amax()))
-            return false;
+            return fail(1, f);
         }
       }
     for (int f = 0; f < F2; f++) {
@@ -460,10 +512,10 @@ int build_devparams(HostParams& hp, DevParams& dp) {
           rbits = (int32_t)x2.m;
           xs2 = x2.xs;
         } else {
-          if (s2[f].amax() >= (1 << 24) || s4[f].amax() >= (1 << 24)) return false;
-          if (!choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f], nullptr, 128, s2[f].amax()) ||
-              !choose_reciprocal(hp.l4_factor[f], &sp.l4_r[f], nullptr, 128, s4[f].amax()))
-            return false;
+          if (s2[f].amax() >= (1 << 24) || !choose_reciprocal(hp.l2_factor[f], &dp.l2_r[f], nullptr, 128, s2[f].amax()))
+            return fail(2, f);
+          if (s4[f].amax() >= (1 << 24) || !choose_reciprocal(hp.l4_factor[f], &sp.l4_r[f], nullptr, 128, s4[f].amax()))
+            return fail(4, f);
           std::memcpy(&rbits, &dp.l2_r[f], 4);
         }
         sp.l2_tpar[f] = (v4i){PBIAS_TAIL + t2, dp.l2_offm[f], rbits, xs2};
@@ -484,10 +536,10 @@ int build_devparams(HostParams& hp, DevParams& dp) {
           sp.l4_xs[f] = x4.xs;
         } else {
           int32_t m2, m4;
-          if (s2[f].amax() >= (1 << 22) || s4[f].amax() >= (1 << 22)) return false;
-          if (!choose_floor_form(f2, 127, s2[f].amax(), &m2, &sp.l2n_r[f], &sp.l2n_c[f]) ||
-              !choose_floor_form(f4, 1024, s4[f].amax(), &m4, &sp.l4n_r[f], &sp.l4n_c[f]))
-            return false;
+          if (s2[f].amax() >= (1 << 22) || !choose_floor_form(f2, 127, s2[f].amax(), &m2, &sp.l2n_r[f], &sp.l2n_c[f]))
+            return fail(2, f);
+          if (s4[f].amax() >= (1 << 22) || !choose_floor_form(f4, 1024, s4[f].amax(), &m4, &sp.l4n_r[f], &sp.l4n_c[f]))
+            return fail(4, f);
           sp.l2n_ci[f] = m2 + o2;
           sp.l4n_ci[f] = m4 + o4;
         }
@@ -524,27 +576,6 @@ int build_devparams(HostParams& hp, DevParams& dp) {
       std::memcpy(&dp.l1_wfrag_ct[t][lane], bytes, 16);
     }
   }
-  // layer 2: A operand = banded weights; row i <-> shift n(i) so that lane (c, h) register r
-  // holds output shift 16h + r (two complete pool-8 windows per lane).  PL: layer-1 row layout,
-  // 2 = parity-split planes (C <= 32, either input layout), 1 = natural order (64 channels).
-  auto l2_bands = [&](int PL, v4i (*afrag)[3][64]) {
-    for (int f = 0; f < F2; f++)
-      for (int s = 0; s < 3; s++)
-        for (int lane = 0; lane < 64; lane++) {
-          const int i = lane & 31, hh = lane >> 5;
-          const int n = 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
-          int8_t bytes[16];
-          for (int jj = 0; jj < 16; jj++) {
-            const int kq = 32 * s + 16 * hh + jj;  // K-slot
-            // position in the 96-byte row window.  PL == 2: lane half hh reads
-            // parity plane hh, bytes 16s .. 16s+15 of the block's window; PL == 1: natural order.
-            const int kp = PL == 2 ? 2 * (16 * s + jj) + hh : kq;
-            const int idx = kp - n - 1;            // tap (torch order)
-            bytes[jj] = (int8_t)((idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0);
-          }
-          std::memcpy(&afrag[f][s][lane], bytes, 16);
-        }
-  };
   // layer-2 tail bands (forward_wg.hpp, layer2_tail_mfma): filter pair w = filters 2w, 2w+1;
   // lane (m, g) of K-step s holds K-slots 64 s + 16 g + jj = chunk kap = 4 s + g, byte jj, which
   // is chunk mq = kap - 6 kf of filter kf = kap / 6; its window position q (tail_q) meets tap
@@ -564,7 +595,7 @@ int build_devparams(HostParams& hp, DevParams& dp) {
           std::memcpy(&tfrag[w][s][lane], bytes, 16);
         }
   };
-  l2_bands(P, dp.l2_afrag);
+  l2_bands(hp, P, dp.l2_afrag);
   l2_tail_bands(P, dp.l2t_afrag);
   SmallParams& sp = dp.sp;
   // layer 3: net_l3_weight is stored flipped (true convolution); torch order = reversed.  A
@@ -611,25 +642,111 @@ int build_devparams(HostParams& hp, DevParams& dp) {
   return NET_OK;
 }
 
+// ---- general-geometry parameter image (forward_gen.hpp) ------------------------------------
+// Every network gen_net_header.py emits with F1 = F2 = 16: C <= 64, 64 <= T <= gen::TMAX,
+// 1 <= N <= gen::NMAX.  Exact integer division at every requant (xdiv), so the same range checks
+// as the specialised image decide NET_ERR_RANGE and nothing else can fail.
+int build_genparams(HostParams& hp, gen::GenParams& gp) {
+  const Dims& d = hp.d;
+  if (d.F1 != F2 || d.F2 != F2 || d.D != 1) return NET_ERR_UNSUPPORTED;
+  if (d.C < 1 || d.C > 64 || d.T < 64 || d.T > gen::TMAX || d.N < 1 || d.N > gen::NMAX) return NET_ERR_UNSUPPORTED;
+  Ranges rg;
+  if (const int rc = check_ranges(hp, rg)) return rc;
+  std::memset(&gp, 0, sizeof(gp));
+  const int C = d.C, CA = d.C_ALIGN(), T8 = d.T8(), T64 = d.T64(), T64A = d.T64_ALIGN();
+  gp.C = C;
+  gp.T = d.T;
+  gp.N = d.N;
+  gp.T8 = T8;
+  gp.T64 = T64;
+  gp.T64A = T64A;
+  gp.NB1 = (d.T + 15) / 16;
+  const int NB2 = (8 * T8 + 31) / 32;  // layer-2 column blocks of 32 outputs
+  gp.MT = (NB2 + 31) / 32;
+  gp.rb = hp.reorder_bn ? 1 : 0;
+  gp.lo = hp.clip_balanced ? -127 : -128;
+  gp.xstride = (int)(((size_t)C * d.T + 15) / 16 * 16);
+  // layer 1: lane (filter j, K group g) holds channels 16 g .. 16 g + 15 (zero past C)
+  for (int lane = 0; lane < 64; lane++) {
+    const int j = lane & 15, g = lane >> 4;
+    int8_t bytes[16];
+    for (int i = 0; i < 16; i++) {
+      const int c = 16 * g + i;
+      bytes[i] = c < C ? hp.l1_weight_align[(size_t)j * CA + c] : 0;
+    }
+    std::memcpy(&gp.l1_b[lane], bytes, 16);
+  }
+  for (int f = 0; f < F2; f++) {
+    const XDiv x1 = xdiv_consts(hp.l1_factor[f]);
+    gp.l1_off[f] = hp.l1_offset[f];
+    gp.l1_m[f] = x1.m;
+    gp.l1_xs[f] = x1.xs;
+    // layers 2 and 4: REORDER_BN pools max(v, -(off >> 3)) and divides by factor; the plain
+    // branches divide each element by factor >> 3 after adding offset >> 3
+    const bool rb = hp.reorder_bn;
+    const XDiv x2 = xdiv_consts(rb ? hp.l2_factor[f] : hp.l2_factor[f] >> 3);
+    gp.l2_thr[f] = -(hp.l2_offset[f] >> 3);
+    gp.l2_off[f] = rb ? hp.l2_offset[f] : hp.l2_offset[f] >> 3;
+    gp.l2_m[f] = x2.m;
+    gp.l2_xs[f] = x2.xs;
+    const XDiv x4 = xdiv_consts(rb ? hp.l4_factor[f] : hp.l4_factor[f] >> 3);
+    gp.sg.l4_thr[f] = -(hp.l4_offset[f] >> 3);
+    gp.sg.l4_off[f] = rb ? hp.l4_offset[f] : hp.l4_offset[f] >> 3;
+    gp.sg.l4_m[f] = x4.m;
+    gp.sg.l4_xs[f] = x4.xs;
+    std::memcpy(gp.sg.l4_w[f], &hp.l4_weight[(size_t)f * F2], 16);
+    // layer 3: torch-order taps W3t[j] = net_l3_weight[f][15 - j] (stored flipped); output phase k
+    // of a 4-output group meets window byte q with tap q - k - 1
+    for (int k = 0; k < 4; k++) {
+      int8_t w[32] = {0};
+      for (int q = 0; q < 20; q++) {
+        const int j = q - k - 1;
+        w[q] = (j >= 0 && j < 16) ? hp.l3_weight[(size_t)f * 16 + 15 - j] : 0;
+      }
+      std::memcpy(gp.sg.l3_w[f][k], w, 32);
+    }
+  }
+  l2_bands(hp, 1, gp.l2_a);
+  const XDiv x3 = xdiv_consts(hp.l3_factor), x5 = xdiv_consts(hp.l5_factor);
+  gp.l3_m = x3.m;
+  gp.l3_xs = x3.xs;
+  gp.l5_m = x5.m;
+  gp.l5_xs = x5.xs;
+  for (int n = 0; n < d.N; n++) {
+    gp.l5_b[n] = hp.l5_bias[n];
+    for (int k = 0; k < F2; k++)
+      for (int v = 0; v < T64; v++) gp.l5_w[n][k * T64A + v] = hp.l5_weight[((size_t)n * F2 + k) * T64A + v];
+  }
+  return NET_OK;
+}
+
 // ---- compiled configurations --------------------------------------------------------------
 // Three shapes: 22 x 1125 (BCI-IV-2a: configs A, B, D, E), 64 x 1000 (config C) and 64 x 480 (the
 // reference's PhysioNet MMMI edgeEEGNet, QuantLab/PhysionetMMMI/config_INQ.json), each compiled
 // with and without -DREORDER_BN, with both clip modes and with float or exact requant:
-// wg::Cfg<C, T, RB, CB, CT, FQ, XR>.
+// wg::Cfg<C, T, RB, CB, CT, FQ, XR>.  Every other geometry (and N != 4) runs the general kernels
+// (gen::k_forward<Layout>, run-time dimensions).
 struct Variant {
-  int shape = -1;  // 0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480, -1: unsupported
+  int shape = -1;  // 0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480, 3: general, -1: unsupported
   bool rb = true;  // -DREORDER_BN branches (canonical)
   bool cb = false; // golden-model clip_balanced (clip to [-127, 127])
   bool xr = false; // exact integer division (parameters outside the float requant envelope)
   bool ok() const { return shape >= 0; }
+  bool general() const { return shape == 3; }
 };
 
+// the compiled geometry of (C, T, N), or -1
+int compiled_shape(const Dims& d) {
+  if (d.F1 != F2 || d.F2 != F2 || d.N != N_OUT) return -1;
+  if (d.C == 22 && d.T == 1125) return 0;
+  if (d.C == 64 && d.T == 1000) return 1;
+  if (d.C == 64 && d.T == 480) return 2;
+  return -1;
+}
+
 Variant variant_of(const HostParams& hp) {
-  const Dims& d = hp.d;
   Variant v;
-  if (d.C == 22 && d.T == 1125) v.shape = 0;
-  else if (d.C == 64 && d.T == 1000) v.shape = 1;
-  else if (d.C == 64 && d.T == 480) v.shape = 2;
+  v.shape = hp.general ? 3 : compiled_shape(hp.d);
   v.rb = hp.reorder_bn;
   v.cb = hp.clip_balanced;
   v.xr = hp.xr;
@@ -676,9 +793,25 @@ size_t trial_stride(const Dims& d) { return ((size_t)d.C * d.T + 15) / 16 * 16; 
 constexpr size_t MAX_IMAGES = 8;
 constexpr size_t MAX_STREAMS = 16;
 
+// A parameter image as uploaded: a wg DevParams (compiled geometries) or a gen::GenParams.
+struct Image {
+  std::shared_ptr<const void> data;
+  size_t bytes = 0;
+  bool same(const Image& o) const {
+    return data == o.data || (bytes == o.bytes && std::memcmp(data.get(), o.data.get(), bytes) == 0);
+  }
+};
+template <class P>
+Image make_image(std::shared_ptr<P> p) {
+  Image im;
+  im.bytes = sizeof(P);
+  im.data = std::move(p);
+  return im;
+}
+
 struct DevImage {
-  std::shared_ptr<const DevParams> host;  // what was uploaded
-  DevParams* dev = nullptr;
+  Image host;                             // what was uploaded
+  void* dev = nullptr;
   uint64_t used = 0;                      // DeviceState::tick at the last selection
   bool pinned = false;                    // captured into a graph (or too many streams): kept
   std::vector<std::pair<hipStream_t, hipEvent_t>> last;  // the last launch per stream
@@ -687,7 +820,7 @@ struct DevImage {
 struct DeviceState {
   std::mutex mu;
   uint64_t gen = 0;             // params generation of `cur`
-  DevParams* cur = nullptr;     // device copy of that generation
+  void* cur = nullptr;          // device copy of that generation (DevParams or gen::GenParams)
   std::vector<DevImage> images; // the copies uploaded to this device
   uint64_t tick = 0;
   int8_t* d_in = nullptr;       // single-trial scratch
@@ -701,7 +834,7 @@ struct DeviceState {
 
 std::mutex g_mu;
 std::shared_ptr<const HostParams> g_host;
-std::shared_ptr<const DevParams> g_dev;
+Image g_img;
 uint64_t g_gen = 0;
 DeviceState g_devs[MAX_DEVICES];
 std::atomic<int> g_single_device{0};  // net_set_device (read by every single-trial call)
@@ -737,13 +870,13 @@ struct DeviceGuard {  // makes `dev` current and restores the caller's device; e
 
 struct Snapshot {
   std::shared_ptr<const HostParams> host;
-  std::shared_ptr<const DevParams> dev;
+  Image img;
   uint64_t gen;
 };
 
 Snapshot snapshot() {
   std::lock_guard<std::mutex> lk(g_mu);
-  return Snapshot{g_host, g_dev, g_gen};
+  return Snapshot{g_host, g_img, g_gen};
 }
 
 void free_image(DevImage& im) {
@@ -820,7 +953,7 @@ int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
   }
   if (ds.gen != s.gen || !ds.cur) {
     for (DevImage& im : ds.images)  // a set loaded before: its copy is still there, unchanged
-      if (im.host == s.dev || std::memcmp(im.host.get(), s.dev.get(), sizeof(DevParams)) == 0) {
+      if (im.host.same(s.img)) {
         ds.cur = im.dev;
         ds.gen = s.gen;
         im.used = ++ds.tick;
@@ -828,11 +961,11 @@ int ensure_device(DeviceState& ds, int dev, const Snapshot& s) {
       }
     evict_idle(ds);
     DevImage im;
-    im.host = s.dev;
+    im.host = s.img;
     im.used = ++ds.tick;
-    hipError_t e = hipMalloc((void**)&im.dev, sizeof(DevParams));
+    hipError_t e = hipMalloc(&im.dev, s.img.bytes);
     if (e != hipSuccess) return hip_err(e);
-    e = hipMemcpy(im.dev, s.dev.get(), sizeof(DevParams), hipMemcpyHostToDevice);
+    e = hipMemcpy(im.dev, s.img.data.get(), s.img.bytes, hipMemcpyHostToDevice);
     g_uploads++;
     if (t_enqueueing) g_uploads_enqueue++;
     if (e != hipSuccess) {
@@ -893,17 +1026,67 @@ int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_
   return hip_err(hipGetLastError());
 }
 
-// layout: 0 time-major int8, 1 channel-major int8, 2 channel-major float32 (scale qs)
-int launch_forward(const Variant& v, DeviceState& ds, const DevParams* p, const int8_t* x, int8_t* y,
+// General path: dynamic LDS from the run-time dimensions (gen::carve_of); the occupancy of each
+// (kernel, LDS size) is queried once.  Kernels may take more than the default 64 KB of dynamic LDS.
+template <class Kern>
+int gen_blocks_per_cu(Kern k, int lds) {
+  static std::mutex mu;
+  static std::vector<std::pair<int, int>> cache;  // (lds, blocks per CU)
+  static bool attr = false;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  for (const auto& c : cache)
+    if (c.first == lds) return c.second;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, gen::NT, (size_t)lds) != hipSuccess || n < 1) n = 1;
+  cache.emplace_back(lds, n);
+  return n;
+}
+
+template <int L>
+int launch_gen_t(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
+                 hipStream_t st, int32_t* info, float qs) {
+  const int lds = gen::carve_of(hg.T8, hg.T64A, hg.NB1, hg.MT, L != gen::TM).bytes;
+  const size_t cap = (size_t)ds.cus * (size_t)gen_blocks_per_cu(gen::k_forward<L>, lds);
+  const int grid = (int)(B < cap ? B : cap);
+  if (info) { info[0] = grid; info[1] = gen::NT; info[2] = lds; return NET_OK; }
+  if (B == 0) return NET_OK;
+  const float qy = qs > 0.0f ? 1.0f / qs : 0.0f;  // RN(1 / scale), as the specialised float kernels
+  hipLaunchKernelGGL(gen::k_forward<L>, dim3(grid), dim3(gen::NT), (size_t)lds, st, (const gen::GenParams*)p, x, y,
+                     (int)B, qs, qy);
+  return hip_err(hipGetLastError());
+}
+
+// layout: 0 time-major int8, 1 channel-major int8, 2 channel-major float32 (scale qs).  himg: the
+// host copy of the image p points to (the general path reads its dimensions).
+int launch_forward(const Variant& v, const void* himg, DeviceState& ds, const void* p, const int8_t* x, int8_t* y,
                    size_t B, hipStream_t st, int32_t* info = nullptr, int layout = 0, float qs = 0.0f) {
-  auto f = [&](auto k) { return launch_forward_t<decltype(k)>(ds, p, x, y, B, st, info, qs); };
+  if (v.general()) {
+    const gen::GenParams& hg = *(const gen::GenParams*)himg;
+    if (layout == 2) return launch_gen_t<gen::F32>(ds, hg, p, x, y, B, st, info, qs);
+    if (layout == 1) return launch_gen_t<gen::CT>(ds, hg, p, x, y, B, st, info, qs);
+    return launch_gen_t<gen::TM>(ds, hg, p, x, y, B, st, info, qs);
+  }
+  const DevParams* dp = (const DevParams*)p;
+  auto f = [&](auto k) { return launch_forward_t<decltype(k)>(ds, dp, x, y, B, st, info, qs); };
   if (layout == 2) return dispatch<true, true>(v, f);
   return layout == 1 ? dispatch<true, false>(v, f) : dispatch<false, false>(v, f);
 }
 
-int launch_layer(const Variant& v, const DevParams* p, const int8_t* in, int8_t* out, int stage, hipStream_t st) {
+int launch_layer(const Variant& v, const void* himg, const void* p, const int8_t* in, int8_t* out, int stage,
+                 hipStream_t st) {
+  if (v.general()) {
+    const gen::GenParams& hg = *(const gen::GenParams*)himg;
+    const int lds = gen::carve_of(hg.T8, hg.T64A, hg.NB1, hg.MT, false).bytes;
+    (void)gen_blocks_per_cu(gen::k_layer, lds);  // the LDS attribute
+    hipLaunchKernelGGL(gen::k_layer, dim3(1), dim3(gen::NT), (size_t)lds, st, (const gen::GenParams*)p, in, out, stage);
+    return hip_err(hipGetLastError());
+  }
   return dispatch(v, [&](auto k) {
-    hipLaunchKernelGGL(wg::k_layer<decltype(k)>, dim3(1), dim3(wg::NTHREADS), 0, st, p, in, out, stage);
+    hipLaunchKernelGGL(wg::k_layer<decltype(k)>, dim3(1), dim3(wg::NTHREADS), 0, st, (const DevParams*)p, in, out, stage);
     return hip_err(hipGetLastError());
   });
 }
@@ -961,9 +1144,9 @@ int run_single(int stage, const int8_t* in, int8_t* out) {
   if (e != hipSuccess) return hip_err(e);
 #endif
   if (stage == 0)
-    rc = launch_forward(v, ds, ds.cur, kin, kout, 1, ds.st);
+    rc = launch_forward(v, s.img.data.get(), ds, ds.cur, kin, kout, 1, ds.st);
   else
-    rc = launch_layer(v, ds.cur, kin, kout, stage, ds.st);
+    rc = launch_layer(v, s.img.data.get(), ds.cur, kin, kout, stage, ds.st);
   if (rc) {
     (void)hipStreamSynchronize(ds.st);  // a copy may still read the staging
     return rc;
@@ -1045,18 +1228,46 @@ const char* net_error_string(int code) {
   }
 }
 
-int net_params_load(const void* blob, size_t len) {
-  auto hp = std::make_shared<HostParams>();
-  int rc = parse_blob(blob, len, *hp);
-  if (rc) return rc;
-  if (!variant_of(*hp).ok()) return NET_ERR_UNSUPPORTED;
-  auto dp = std::make_shared<DevParams>();
-  rc = build_devparams(*hp, *dp);
-  if (rc) return rc;
+namespace {
+// Builds the device image of a parsed set and makes it current: the compiled kernels when its
+// geometry has them, the general kernels otherwise.
+int install(std::shared_ptr<HostParams> hp) {
+  Image img;
+  hp->general = g_force_general.load() != 0 || compiled_shape(hp->d) < 0;
+  if (hp->general) {
+    auto gp = std::make_shared<gen::GenParams>();
+    if (const int rc = build_genparams(*hp, *gp)) return rc;
+    img = make_image(gp);
+  } else {
+    auto dp = std::make_shared<DevParams>();
+    if (const int rc = build_devparams(*hp, *dp)) return rc;
+    img = make_image(dp);
+  }
   std::lock_guard<std::mutex> lk(g_mu);
   g_host = hp;
-  g_dev = dp;
+  g_img = img;
   g_gen++;
+  return NET_OK;
+}
+}  // namespace
+
+int net_params_load(const void* blob, size_t len) {
+  auto hp = std::make_shared<HostParams>();
+  const int rc = parse_blob(blob, len, *hp);
+  if (rc) return rc;
+  return install(hp);
+}
+
+int net_params_info(int32_t* info) {
+  if (!info) return NET_ERR_INVALID;
+  Snapshot s = snapshot();
+  for (int i = 0; i < 4; i++) info[i] = 0;
+  if (!s.host) return NET_ERR_NO_PARAMS;
+  const HostParams& hp = *s.host;
+  info[0] = hp.general ? NET_PATH_GENERAL : hp.xr ? NET_PATH_EXACT : NET_PATH_FLOAT;
+  info[1] = hp.general ? 0 : hp.xr_layer;
+  info[2] = hp.general || !hp.xr ? -1 : hp.xr_filter;
+  info[3] = hp.general ? -1 : compiled_shape(hp.d);
   return NET_OK;
 }
 
@@ -1064,7 +1275,7 @@ void net_params_unload(void) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     g_host.reset();
-    g_dev.reset();
+    g_img = Image();
     g_gen++;
   }
   // free every device copy once the launches that may read it have finished
@@ -1139,7 +1350,7 @@ int batch_async_s(const Snapshot& s, const int8_t* x, int8_t* y, size_t B, int d
   if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
-  rc = launch_forward(v, ds, ds.cur, x, y, B, (hipStream_t)stream, nullptr, layout, qs);
+  rc = launch_forward(v, s.img.data.get(), ds, ds.cur, x, y, B, (hipStream_t)stream, nullptr, layout, qs);
   if (rc == NET_OK && B) note_launch(ds, (hipStream_t)stream);
   return rc;
 }
@@ -1276,6 +1487,11 @@ int mibminet_test_pool_consts(int32_t off, int32_t layer, int32_t* thr, int32_t*
   return NET_OK;
 }
 
+int mibminet_test_force_general(int on) {
+  g_force_general.store(on ? 1 : 0);
+  return NET_OK;
+}
+
 int mibminet_test_params_xr(void) {
   Snapshot s = snapshot();
   if (!s.host) return NET_ERR_NO_PARAMS;
@@ -1359,7 +1575,7 @@ int launch_info(size_t B, int device, int32_t* out, bool ct) {
   if (guard.err != hipSuccess) return hip_err(guard.err);
   int rc = ensure_device(ds, device, s);
   if (rc) return rc;
-  return launch_forward(v, ds, nullptr, nullptr, nullptr, B, nullptr, out, ct);
+  return launch_forward(v, s.img.data.get(), ds, nullptr, nullptr, nullptr, B, nullptr, out, ct);
 }
 }  // namespace
 

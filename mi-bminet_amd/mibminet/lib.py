@@ -34,8 +34,9 @@ EXPORTED_SYMBOLS = (
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
     "net_pack_trials_i8", "net_model_compute_batch_multi", "net_model_compute_batch_ct",
     "net_model_compute_batch_multi_ct", "net_launch_info_ct", "net_model_compute_batch_f32",
-    "net_model_compute_batch_ct_sync",
+    "net_model_compute_batch_ct_sync", "net_params_info",
 )
+NET_PATH_FLOAT, NET_PATH_EXACT, NET_PATH_GENERAL = 0, 1, 2
 
 
 class NetError(RuntimeError):
@@ -114,7 +115,11 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_model_compute_batch_multi_ct.restype = i
     L.net_model_compute_batch_ct_sync.argtypes = [vp, vp, sz, i]
     L.net_model_compute_batch_ct_sync.restype = i
+    L.net_params_info.argtypes = [vp]
+    L.net_params_info.restype = i
     # test hooks (include/mibminet_testing.h)
+    L.mibminet_test_force_general.argtypes = [i]
+    L.mibminet_test_force_general.restype = i
     L.mibminet_test_xdiv_host.argtypes = [vp, sz, ctypes.c_int32, vp]
     L.mibminet_test_xdiv_host.restype = i
     L.mibminet_test_xdiv_gpu.argtypes = [ctypes.c_int32, ctypes.c_int64, ctypes.c_int64, vp, i]
@@ -253,6 +258,21 @@ def model_compute_batch_ct_sync(x_ptr: int, y_ptr: int, B: int, device: int = 0)
     """net_model_compute_batch_ct_sync (SURVEY §8(b)'s signature): channel-major [B][C][T] int8
     trials and [B][N] logits, device pointers; waits for completion."""
     _check(load().net_model_compute_batch_ct_sync(x_ptr, y_ptr, B, device), "net_model_compute_batch_ct_sync")
+
+
+def params_info() -> dict:
+    """net_params_info: which kernels the loaded set runs ("float", "exact" or "general"), and for
+    "exact" the first layer / filter whose requant has no proven float form."""
+    arr = (ctypes.c_int32 * 4)()
+    _check(load().net_params_info(arr), "net_params_info")
+    path = {NET_PATH_FLOAT: "float", NET_PATH_EXACT: "exact", NET_PATH_GENERAL: "general"}[arr[0]]
+    return {"path": path, "layer": arr[1], "filter": arr[2], "shape": arr[3]}
+
+
+def force_general(on: bool) -> None:
+    """Test hook (mibminet_test_force_general): later loads run the run-time-dimension kernels
+    even for the compiled geometries."""
+    _check(load().mibminet_test_force_general(1 if on else 0), "mibminet_test_force_general")
 
 
 def params_exact_division() -> bool:

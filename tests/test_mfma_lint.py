@@ -128,7 +128,7 @@ def test_trial_loop_barriers_do_not_drain_prefetch(device_asm):
     and nothing else in these kernels touches m0.  (LDS-DMA serves the 22-channel shapes only: the
     channel-major int8 ring, and the blocks past the VGPR prefetch of time-major plain BN and exact
     division.)"""
-    funcs = {n: ls for n, ls in _functions(device_asm).items() if "k_forward" in n}
+    funcs = {n: ls for n, ls in _functions(device_asm).items() if "2wg9k_forward" in n}
     assert len(funcs) == 72
     n_dma = 0
     for name, lines in funcs.items():
@@ -177,7 +177,7 @@ def test_dma_ring_wait_counts_issued_ops(device_asm):
     least N vector-memory operations follow the trial loop's last fill.  Scratch
     traffic (spills) after the fill only makes the wait stricter."""
     import re
-    funcs = {n: ls for n, ls in _functions(device_asm).items() if "k_forward" in n}
+    funcs = {n: ls for n, ls in _functions(device_asm).items() if "2wg9k_forward" in n}
     checked = 0
     for name, lines in funcs.items():
         fills = [i for i, l in enumerate(lines) if l.startswith("buffer_load_dwordx4") and l.endswith(" lds")]
@@ -222,6 +222,6 @@ def test_layer1_cinit_not_written_near_loads(device_asm):
             hits = cinit_scan.scan(cinit_scan.parse(str(asm)), [])
         finally:
             sys.stdout = old
-    funcs = [n for n in cinit_scan.parse(str(asm)) if "k_forward" in n]
+    funcs = [n for n in cinit_scan.parse(str(asm)) if "2wg9k_forward" in n]
     assert len(funcs) == 72
     assert not [h for h in hits if h[1] == 1], [h for h in hits if h[1] == 1]
