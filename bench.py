@@ -5,7 +5,7 @@ One "step" = one fused forward pass (one kernel launch) over a batch of 65,536 s
 22-channel x 1125-sample int8 trials already resident in HBM (BASELINE config B; with --gpus N
 each rank owns its own 65,536-trial shard: config E's static split, weak scaling, no collectives).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config b22|c64|d22] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config b22|c64|d22|p64|g19|g38|p64l] [--batch B]
 
 For N > 1 launch under ``torch.distributed.run`` (one process per GPU); rank 0 prints ONE JSON
 line.  ``value`` = trials processed by all ranks / max-over-ranks wall time of the K timed steps.
@@ -15,7 +15,9 @@ group is ever created, and nothing collective runs inside the K timed steps: eac
 own steps (host clock around them, HIP events on its launch stream), then the ranks reduce.
 ``roofline.achieved`` = algorithmic bytes per launch (input 22*1125 B + 4 B logits per trial) /
 average kernel duration from HIP events on the launch stream.  ``cpu_baseline`` times the C
-restatement of the reference forward (oracle/, kind "port") on the host cores (rank 0, N = 1).
+restatement of the reference forward (oracle/, kind "port") on the host cores (rank 0, N = 1),
+and its logits on that sample are compared with the timed batch's: ``parity`` = trials checked and
+mismatches; any mismatch makes the run exit non-zero (after printing the line).
 """
 import argparse
 import json
@@ -39,6 +41,10 @@ CONFIGS = {
     "c64": dict(C=64, T=1000, wbits=8, name="C: 64ch x 1000 int8, 4-class"),
     "d22": dict(C=22, T=1125, wbits=4, name="D: 22ch x 1125, int4 weights / int8 acts"),
     "p64": dict(C=64, T=480, wbits=8, name="PhysioNet MMMI: 64ch x 480 int8, 4-class (not a BASELINE config)"),
+    # geometries without a compiled kernel: the run-time-dimension kernels (forward_gen.hpp)
+    "g19": dict(C=19, T=1125, wbits=8, N=3, name="channel-selected 19ch x 1125 int8, 3-class (general kernels)"),
+    "g38": dict(C=38, T=480, wbits=8, N=2, name="PhysioNet channel-selected 38ch x 480 int8, 2-class (general kernels)"),
+    "p64l": dict(C=64, T=960, wbits=8, N=4, name="PhysioNet MMMI 6 s window: 64ch x 960 int8, 4-class (general kernels)"),
 }
 
 
@@ -61,6 +67,8 @@ def parse():
                     help="synthetic: calibrated seeded weights (the benchmark set, float requant kernels); "
                          "extreme: requant factors and offsets far outside the float envelope "
                          "(ParamSet.synthetic_extreme, the exact integer-division kernels)")
+    ap.add_argument("--force-general", action="store_true",
+                    help="run the run-time-dimension kernels even on a compiled geometry (comparison)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--settle", type=float, default=0.25,
                     help="seconds of untimed launches before the warmup steps (GPU clock ramp)")
@@ -130,7 +138,7 @@ def cpu_baseline(ps, x_dev, seconds):
     sample = x_dev[:n].cpu().numpy()
     t0 = time.perf_counter()
     for _ in range(reps):
-        co.batch(sample, nthreads=threads)
+        logits = co.batch(sample, nthreads=threads)
     dt = time.perf_counter() - t0
     n *= reps
     cpu = "unknown"
@@ -161,7 +169,7 @@ def cpu_baseline(ps, x_dev, seconds):
         dm = time.perf_counter() - tm
         mask = {"value": nm / dm, "unit": "trials/s", "threads": ncpu,
                 "sample": f"{nm} trials, {ncpu} threads under a {quota}-CPU quota, {dm:.1f} s"}
-    return {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
+    return logits, {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
             "sample": f"{n} trials ({reps} pass(es) over the first {n // reps} trials) of the same synthetic batch, C restatement (oracle/oracle.c, -O3) "
                       f"of net_model_compute, {threads} host threads (one per usable CPU: affinity mask "
                       f"{ncpu}, cgroup quota {quota}) on {cpu}, {dt:.1f} s",
@@ -169,6 +177,15 @@ def cpu_baseline(ps, x_dev, seconds):
             "affinity_mask_threads": mask,
             "host_cpus": {"affinity": ncpu, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota,
                           "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}}
+
+
+def logit_parity(y_host, want):
+    """Trials of the timed batch whose logits differ from the oracle's on the same trials
+    (the reference's own exact-logit check around its timed call, test/cl/net/model/cluster.c:44-49)."""
+    n = want.shape[0]
+    bad = np.nonzero(np.any(y_host[:n] != want, axis=1))[0]
+    return {"checked": int(n), "mismatches": int(bad.size), "first_bad": bad[:8].tolist(),
+            "against": "oracle/oracle.c (C restatement of net_model_compute) on the first trials of the timed batch"}
 
 
 def pcie_inclusive(x, y, B, device, sp, stream, reps=5):
@@ -211,21 +228,29 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("gloo", init_method="env://")
 
-    make = ParamSet.synthetic_extreme if a.params == "extreme" else ParamSet.synthetic
-    ps = make(a.seed, C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"],
-              reorder_bn=a.variant != "plain_bn", clip_balanced=a.variant == "clip_balanced")
+    kw = dict(C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"], reorder_bn=a.variant != "plain_bn",
+              clip_balanced=a.variant == "clip_balanced")
+    if a.params == "extreme":
+        ps = ParamSet.synthetic_extreme(a.seed, **kw)
+    else:
+        ps = ParamSet.synthetic(a.seed, N=cfg.get("N", 4), **kw)
+    if a.force_general and not STUB:
+        lib.force_general(True)
     lib.params_load(ps)
+    info_p = {"path": "stub", "layer": 0, "filter": -1, "shape": -1} if STUB else lib.params_info()
     stride = lib.trial_stride()
     B = a.batch
     g = torch.Generator(device=dev)
     g.manual_seed(a.seed * 1000 + rank)
     sync = (lambda: None) if STUB else (lambda: torch.cuda.synchronize(dev))
-    C, T = cfg["C"], cfg["T"]
-    if a.layout == "f32":
+    C, T, N = cfg["C"], cfg["T"], cfg.get("N", 4)
+    if STUB:  # host int8 trials whatever the layout (no device, no library compute)
+        x = torch.randint(-128, 128, (B, stride), dtype=torch.int8, generator=g)
+    elif a.layout == "f32":
         # float EEG whose quantised values spread over the int8 range (scale = 3 sigma)
         xf = torch.randn((B, C, T), dtype=torch.float32, device=dev, generator=g)
         qscale = 3.0
-        x = None if STUB else lib.quantize_input_torch(xf, qscale)  # the same trials as int8, time-major (CPU baseline)
+        x = lib.quantize_input_torch(xf, qscale)  # the same trials as int8, time-major (CPU baseline)
         sync()
     elif a.layout == "ct":
         xc = torch.randint(-128, 128, (B, C, T), dtype=torch.int8, device=dev, generator=g)
@@ -234,7 +259,7 @@ def main():
     else:
         x = torch.randint(-128, 128, (B, stride), dtype=torch.int8, device=dev, generator=g)
         x[:, C * T:] = 0
-    y = torch.empty((B, 4), dtype=torch.int8, device=dev)
+    y = torch.empty((B, N), dtype=torch.int8, device=dev)
     stream = None if STUB else torch.cuda.current_stream(dev)
     sp = None if STUB else stream.cuda_stream
     ct_fn = lib.load().net_model_compute_batch_ct
@@ -242,7 +267,7 @@ def main():
 
     def step():
         if STUB:
-            y.copy_(x[:, :4])  # stand-in work on the host
+            y.copy_(x[:, :N])  # stand-in work on the host
         elif a.layout == "f32":
             rc = f32_fn(xf.data_ptr(), y.data_ptr(), B, qscale, local, sp)
             if rc:
@@ -309,11 +334,12 @@ def main():
         dist.all_gather_object(per_rank, mine)
         elapsed = elapsed_max
 
+    failed = None
     info = {"grid": 0, "threads": 0, "lds_bytes": 0} if STUB else lib.launch_info(B, local, channel_major=a.layout != "tc")
     if rank == 0:
         # N > 1: the slowest rank's kernel average (each rank's is listed under "ranks")
         avg_kernel_s = (max(r["kernel_ms"] for r in per_rank) if per_rank else rank_avg_ms) / 1e3
-        alg_bytes_trial = cfg["C"] * cfg["T"] * (4 if a.layout == "f32" else 1) + 4
+        alg_bytes_trial = cfg["C"] * cfg["T"] * (4 if a.layout == "f32" else 1) + N
         achieved = alg_bytes_trial * B / avg_kernel_s / 1e9
         traffic = None
         try:
@@ -354,13 +380,18 @@ def main():
                        "grid": info["grid"], "threads": info["threads"], "lds_bytes": info["lds_bytes"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d,FQ=%d,XR=%d>>" % (
+                         "kernel": ("gen::k_forward<%s> (C=%d, T=%d, N=%d at run time)" % (
+                             {"tc": "TM", "ct": "CT", "f32": "F32"}[a.layout], C, T, N)
+                             if info_p["path"] == "general" else
+                             "k_forward<Cfg<%d,%d,RB=%d,CB=%d,CT=%d,FQ=%d,XR=%d>>" % (
                              cfg["C"], cfg["T"], a.variant != "plain_bn", a.variant == "clip_balanced",
-                             a.layout != "tc", a.layout == "f32", lib.params_exact_division()),
+                             a.layout != "tc", a.layout == "f32", info_p["path"] == "exact")),
                          "avg_kernel_ms": avg_kernel_s * 1e3,
                          "alg_bytes_per_launch": alg_bytes_trial * B},
             "cpu_baseline": None,
-            "requant": "exact integer division" if lib.params_exact_division() else "float (proven exact)",
+            "requant": "float (proven exact)" if info_p["path"] == "float" else "exact integer division",
+            "kernel_path": info_p,
+            "parity": None,
         }
         if dist:
             out["ranks"] = {"world_size": dist.get_world_size(), "backend": dist.get_backend(),
@@ -369,14 +400,25 @@ def main():
                                     "wall time; coordination over gloo (host) only, no RCCL"}
         if STUB:
             out["stub"] = "MIB_BENCH_STUB: host stand-in step, bookkeeping test only, not a measurement"
+            yh = y.numpy().copy()
+            if os.environ.get("MIB_BENCH_STUB_CORRUPT") == "1":
+                yh[B // 2, 0] ^= 1  # the parity check's failure path (tests/test_bench_cpu.py)
+            out["parity"] = logit_parity(yh, x[:, :N].numpy())
+            out["parity"]["against"] = "stub stand-in"
         if a.pcie and not STUB:
             out["pcie_inclusive"] = pcie_inclusive(x, y, B, local, sp, stream)
         if world == 1 and not a.no_cpu_baseline and not STUB:
-            out["cpu_baseline"] = cpu_baseline(ps, x, a.cpu_seconds)
+            want, out["cpu_baseline"] = cpu_baseline(ps, x, a.cpu_seconds)
+            out["parity"] = logit_parity(y[: want.shape[0]].cpu().numpy(), want)
         print(json.dumps(out), flush=True)
+        if out["parity"] and out["parity"]["mismatches"]:
+            failed = "bench.py: the timed batch's logits differ from the oracle's on %d of %d trials" % (
+                out["parity"]["mismatches"], out["parity"]["checked"])
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+    if failed:
+        raise SystemExit(failed)
 
 
 if __name__ == "__main__":

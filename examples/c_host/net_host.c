@@ -16,6 +16,11 @@
  *   net_host bench <params.blob> [B=65536] [steps=50]
  *       Times `steps` back-to-back net_model_compute_batch_async launches over B resident
  *       random trials with HIP events and prints one line of trials/s.
+ *
+ * Built with -DMIB_NET_H against a generated net.h / net.c (the reference's weight globals,
+ * gen_net_header.py; net_host_b22 / net_host_g19 in the Makefile), <params.blob> may be "-": the
+ * parameters then come from the linked arrays through net_params_load_arrays
+ * (include/mibminet_net_h.h), as the reference's callers link them (src/cl/cluster.c:38).
  */
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
@@ -24,6 +29,10 @@
 #include <string.h>
 
 #include "mibminet.h"
+#ifdef MIB_NET_H
+#include "net.h"
+#include "mibminet_net_h.h"
+#endif
 
 static void* read_file(const char* path, size_t* len) {
     FILE* f = fopen(path, "rb");
@@ -47,6 +56,18 @@ static void* read_file(const char* path, size_t* len) {
 }
 
 static int load_params(const char* path, int32_t dims[7]) {
+#ifdef MIB_NET_H
+    if (!strcmp(path, "-")) {  /* the linked net.c: no blob, no file */
+        const int rc = mibminet_load_net_h();
+        if (rc) {
+            fprintf(stderr, "net_params_load_arrays: %s\n", net_error_string(rc));
+            return 1;
+        }
+        net_params_dims(dims);
+        printf("parameters: linked net.c (C=%d T=%d N=%d)\n", NET_C, NET_T, NET_N);
+        return 0;
+    }
+#endif
     size_t len = 0;
     void* blob = read_file(path, &len);
     if (!blob) return 1;

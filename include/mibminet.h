@@ -75,7 +75,7 @@ int net_last_error(void);
 
 /* ---- parameters (replace the link-time globals of the generated net.h/net.c) ------------- */
 
-/* Load a parameter blob (format: mi-bminet_amd/mibminet/params.py, ParamSet.to_blob): the
+/* Load a parameter blob (format: net_params_load_arrays below; mibminet/params.py, ParamSet.to_blob): the
  * net.h arrays net_l1_factor ... net_l5_weight with their dimensions, int8 or packed int4
  * weights, and the build variant (flag bit 0: -DREORDER_BN, the canonical build; clear: the plain
  * BN branches of layer2.c:139-210 / layer4.c:91-133.  Flag bit 1: clip every requantised output to
@@ -109,13 +109,52 @@ int net_params_load(const void* blob, size_t len);
  * info[0] = NET_PATH_FLOAT (compiled geometry, float requant proven exact on every reachable
  * value), NET_PATH_EXACT (compiled geometry, exact integer division at layers 1, 2 and 4: about
  * 1.5x the float kernels' time on 22 x 1125) or NET_PATH_GENERAL (run-time-dimension kernels,
- * exact division throughout); info[1] = the layer (1, 2 or 4) of the first requant that has no
+ * float or exact requant as info[4] says); info[1] = the layer (1, 2 or 4) of the first requant that has no
  * proven float form (NET_PATH_EXACT), else 0; info[2] = its filter, else -1; info[3] = the
- * compiled geometry (0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480), -1 on the general path. */
+ * compiled geometry (0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480), -1 on the general path; info[4] = 1
+ * when the set divides exactly at layers 1-4 (NET_PATH_EXACT, or NET_PATH_GENERAL without a proven
+ * float form for every requant), 0 when it runs the proven float requant.  info holds 5 entries. */
 #define NET_PATH_FLOAT 0
 #define NET_PATH_EXACT 1
 #define NET_PATH_GENERAL 2
 int net_params_info(int32_t* info);
+
+/* The reference's generated globals (edge-eegnet_wolf/data/gen_net_header.py:78-224, written by
+ * python_utils/header_file.py as src/cl/net/net.{h,c}), by pointer, in their own layouts: a C host
+ * that links the reference's net.c loads them with net_params_load_arrays and needs no blob file
+ * and no Python.  include/mibminet_net_h.h fills this struct from the NET_* macros and net_l*
+ * arrays of an included net.h (and the build variant from -DREORDER_BN, as the reference's
+ * Makefile selects it).  Weights are int8, as net.c holds them. */
+typedef struct {
+    int32_t C, T, F1, F2, D, N;         /* NET_C, NET_T, NET_F1, NET_F2, NET_D, NET_N */
+    uint32_t flags;                     /* NET_FLAG_REORDER_BN | NET_FLAG_CLIP_BALANCED (blob flag bits) */
+    const int32_t* l1_factor;           /* net_l1_factor [F2] */
+    const int32_t* l1_offset;           /* net_l1_offset [F2] */
+    const int8_t* l1_weight_align;      /* net_l1_weight_align [F2][C_ALIGN], zero pad */
+    const int32_t* l2_factor;           /* net_l2_factor [F2] (pool 8 folded in) */
+    const int32_t* l2_offset;           /* net_l2_offset [F2] */
+    const int8_t* l2_weight_reverse;    /* net_l2_weight_reverse [F2][64] (torch order) */
+    int32_t l3_factor;                  /* NET_L3_FACTOR */
+    const int8_t* l3_weight;            /* net_l3_weight [F2][16] (flipped) */
+    const int32_t* l4_factor;           /* net_l4_factor [F2] */
+    const int32_t* l4_offset;           /* net_l4_offset [F2] */
+    const int8_t* l4_weight;            /* net_l4_weight [F2][F2] */
+    int32_t l5_factor;                  /* NET_L5_FACTOR */
+    const int8_t* l5_bias;              /* net_l5_bias [N] */
+    const int8_t* l5_weight;            /* net_l5_weight [N][F2 * T64_ALIGN], zero pad per row */
+} net_arrays_t;
+#define NET_FLAG_REORDER_BN 1u
+#define NET_FLAG_CLIP_BALANCED 2u
+
+/* Loads the arrays of `a` exactly as net_params_load loads a blob holding them (same checks,
+ * codes and device images; the arrays are copied, so they may go away after the call).  A blob
+ * is the same fields serialised: a 64-byte header "MIBMINET", then uint32 version = 1, C, T, F1,
+ * F2, D, N, weight_bits (8, or 4 for packed nibbles: element 2i in the low nibble of byte i),
+ * l2_taps = 64, l3_taps = 16, flags, zero to byte 64; then l1_factor, l1_offset, l1_weight_align,
+ * l2_factor, l2_offset, l2_weight_reverse, l3_factor, l3_weight, l4_factor, l4_offset, l4_weight,
+ * l5_factor, l5_bias, l5_weight in that order, little endian, each section zero-padded to a
+ * multiple of 4 bytes (mibminet/params.py, ParamSet.to_blob, writes it). */
+int net_params_load_arrays(const net_arrays_t* a);
 
 /* dims[0..6] = C, T, F1, F2, N, weight_bits, loaded(0/1). */
 int net_params_dims(int32_t* dims);

@@ -70,6 +70,10 @@ int mibminet_test_params_xr(void);
  * checked against the oracle on the same set; 0 restores the normal choice. */
 int mibminet_test_force_general(int on);
 
+/* FNV-1a digest of the loaded set's device parameter image (the bytes uploaded to every device):
+ * equal digests mean the two loads produce the same kernels' inputs. */
+int mibminet_test_image_digest(uint64_t* digest);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,8 +27,11 @@
 //           transposed [u][f] (the reference's flip is index math).   (reference: layer3.c:49-79)
 //   layer4  16x16 pointwise on the VALU (v_dot4), ReLU-pool and requant.  (reference: layer4.c:51-149)
 //   layer5  N-class linear layer: one wave per class, v_dot4 + a wave reduction.  (reference: layer5.c:43-89)
-// Every requantisation is exact integer division (xdiv, forward_common.hpp), so every parameter
-// set the reference's int32 arithmetic defines runs here without a float envelope.
+// Requantisation as in the compiled kernels: where the host proves the float form exact on every
+// reachable value (mibminet.hip: choose_reciprocal, choose_floor_form) the XR = false build runs
+// it; any requant without a proven float form sends the set to the XR = true build, exact
+// integer division (xdiv, forward_common.hpp) at layers 1-4.  Layer 5 always divides exactly (its
+// sums pass 2^24 at T = 4096).  CB: balanced clipping ([-127, 127], golden model clip_balanced).
 #pragma once
 #include "forward_wg.hpp"
 
@@ -51,8 +54,12 @@ struct SmallG {
   int l4_w[F2][4];        // layer 4: weight row k, 16 bytes
   int l4_thr[F2];         // REORDER_BN: -(offset >> 3); plain: unused
   int l4_off[F2];         // REORDER_BN: offset; plain: offset >> 3
-  unsigned l4_m[F2];      // xdiv magic of factor (plain: factor >> 3)
+  unsigned l4_m[F2];      // XR: xdiv magic of factor (plain: factor >> 3)
   int l4_xs[F2];
+  float l4_r[F2];         // float form: reciprocal (REORDER_BN) / floor-form r (plain)
+  float l4_c[F2];         // plain floor form: c
+  int l4_ci[F2];          // plain floor form: magic bits + offset >> 3
+  int pad[4];
 };
 static_assert(sizeof(SmallG) % 16 == 0, "SmallG is copied in 16-byte pieces");
 
@@ -60,19 +67,24 @@ static_assert(sizeof(SmallG) % 16 == 0, "SmallG is copied in 16-byte pieces");
 struct GenParams {
   int C, T, N, T8;
   int T64, T64A, NB1, MT;       // NB1: layer-1 blocks of 16 samples; MT: layer-2 tiles of 1024 outputs
-  int rb, lo, xstride, pad0;    // REORDER_BN branches; lower clip bound; time-major trial stride
+  int rb, lo, xstride, xr;      // REORDER_BN branches; lower clip bound; time-major trial stride;
+                                // exact division (no proven float form for some requant)
   unsigned l3_m;
   int l3_xs;
   unsigned l5_m;
   int l5_xs;
+  float l3_r, l3_c;             // float form of layer 3: magic C-init, fma(acc bits, r, c)
+  int pad1[2];
   v4i l1_b[64];                 // layer-1 B operand: lane (filter lane & 15, g) = W1[f][16 g .. +15]
-  int l1_off[F2];
-  unsigned l1_m[F2];
+  int l1_off[F2];               // XR: offset (the MFMA C-init); float: offset + FMAGIC_I
+  unsigned l1_m[F2];            // XR: xdiv magic
   int l1_xs[F2];
-  int l2_thr[F2];               // REORDER_BN: -(offset >> 3); plain: unused
+  float l1_r[F2], l1_c[F2];     // float form: fma(acc bits, r, c) = RN((dot + off) r)
+  int l2_thr[F2];               // REORDER_BN: -(offset >> 3); plain float form: magic bits + offset >> 3
   int l2_off[F2];               // REORDER_BN: offset; plain: offset >> 3
-  unsigned l2_m[F2];            // xdiv magic of factor (plain: factor >> 3)
+  unsigned l2_m[F2];            // XR: xdiv magic of factor (plain: factor >> 3)
   int l2_xs[F2];
+  float l2_r[F2], l2_c[F2];     // float form: reciprocal (REORDER_BN); floor-form r, c (plain)
   int l5_b[NMAX];
   SmallG sg;
   v4i l2_a[F2][3][64];          // layer-2 A operand (banded weights) per filter, K-step and lane
@@ -173,11 +185,33 @@ struct TrK {
 
 // Layer 1: this wave's blocks blk = wave, wave + NW, ... -> y1 rows (position 32 + t).  Loads of
 // U blocks are issued before their MFMAs.
-template <int L>
+// Requant of one layer-1 output (acc = dot + offset, or its float-magic form): exact division
+// (XR) or fma(acc bits, r, c) = RN((dot + off) r), truncated (the host proves it equals C's
+// division on every reachable value).  Both clip to [LO, 127] (the upper bound and -128 by the
+// saturating pack).
+template <bool XR, bool CB>
+__device__ __forceinline__ int rq1(int acc, unsigned m, int xs, float r, float c) {
+  int y = XR ? xdiv(acc, m, xs) : (int)__builtin_fmaf(__int_as_float(acc), r, c);
+  if (XR) y = min(y, 127);
+  return CB ? max(y, -127) : XR ? max(y, -128) : y;
+}
+// four outputs in [-128, 127] (or to be saturated there) -> bytes 0..3
+__device__ __forceinline__ unsigned sat4(int a, int b, int c, int d) {
+  const unsigned lo = __builtin_amdgcn_ashr_pk_i8_i32(a, b, 0), hi = __builtin_amdgcn_ashr_pk_i8_i32(c, d, 0);
+  return (lo & 0xFFFFu) | (hi << 16);
+}
+
+struct L1C {  // a lane's layer-1 constants (filter lane & 15)
+  v4i wf;
+  int off, xs;
+  unsigned m;
+  float r, c;
+};
+
+template <int L, bool XR, bool CB>
 __device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const View& v, int8_t* y1, int y1s,
-                                       int8_t* stg, const v4i& wf, int off, unsigned m, int xs, int wave, int lane,
-                                       float qs, float qy) {
-  const int C = gp->C, T = gp->T, NB1 = gp->NB1, lo = gp->lo;
+                                       int8_t* stg, const L1C& k, int wave, int lane, float qs, float qy) {
+  const int C = gp->C, T = gp->T, NB1 = gp->NB1;
   const int j = lane & 15, g = lane >> 4;
   constexpr int U = L == F32 ? 2 : 4;
   for (int b0 = wave; b0 < NB1; b0 += U * NW) {
@@ -192,13 +226,17 @@ __device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const V
       const int blk = b0 + u * NW;
       if (blk < NB1) {  // wave-uniform
         const v4i a = L == TM ? raw[u] : wg::stage_block<TrK>(raw[u], stg, lane);
-        const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, wf, (v4i){off, off, off, off}, 0, 0, 0);
+        const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, k.wf, (v4i){k.off, k.off, k.off, k.off}, 0, 0, 0);
         // lane column j = filter j, rows 4 g + r = samples 16 blk + 4 g + r
         const int t0 = 16 * blk + 4 * g;
         int y[4];
 #pragma unroll
-        for (int r = 0; r < 4; r++) y[r] = t0 + r < T ? clampq(xdiv(acc[r], m, xs), lo) : 0;
-        *(unsigned*)(y1 + j * y1s + 32 + t0) = pack4(y[0], y[1], y[2], y[3]);
+        for (int r = 0; r < 4; r++) y[r] = rq1<XR, CB>(acc[r], k.m, k.xs, k.r, k.c);
+        if (blk == NB1 - 1) {  // the trial's last block: samples >= T are zero (the xcorr's pad)
+#pragma unroll
+          for (int r = 0; r < 4; r++) y[r] = t0 + r < T ? y[r] : 0;
+        }
+        *(unsigned*)(y1 + j * y1s + 32 + t0) = sat4(y[0], y[1], y[2], y[3]);
       }
     }
   }
@@ -207,10 +245,27 @@ __device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const V
 // Layer 2 (layer2.c:56-118 REORDER_BN, :139-210 plain): the wave's filters 2 wave + fi.  Lane
 // (n, h) of tile mt holds conv outputs 1024 mt + 32 n + 16 h + r (r < 16), i.e. the pool windows
 // u0 = 128 mt + 4 n + 2 h and u0 + 1.
+struct L2C {  // a wave's layer-2 constants (filters 2 wave, 2 wave + 1)
+  v4i af[2][3];
+  int thr[2], off[2], xs[2];
+  unsigned m[2];
+  float r[2], c[2];
+};
+
+// floor form of one plain-branch element (mibminet.hip, choose_floor_form): acc holds the bits of
+// float(M + x) (MFMA C-init M + offset), and bits(fmed3(fma(acc, r, c), K, K + emax)) - bits(K) =
+// clamp(floor(x / fac), 0, emax) = the element after its clip and ReLU
+template <int EMAX>
+__device__ __forceinline__ int floor_el(int acc, float r, float c) {
+  const float g = __builtin_fmaf(__int_as_float(acc), r, c);
+  return __float_as_int(__builtin_amdgcn_fmed3f(g, FMAGIC_F, FMAGIC_F + (float)EMAX)) - FMAGIC_I;
+}
+
+template <bool XR, bool CB>
 __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const int8_t* y1, int y1s, int8_t* y2, int y2s,
-                                       const v4i (&af)[2][3], const int (&thr)[2], const int (&off)[2],
-                                       const unsigned (&m)[2], const int (&xs)[2], int wave, int lane) {
-  const int T8 = gp->T8, MT = gp->MT, lo = gp->lo;
+                                       const L2C& k, int wave, int lane) {
+  constexpr int LO = CB ? -127 : -128;
+  const int T8 = gp->T8, MT = gp->MT;
   const bool rb = gp->rb != 0;
   const int n = lane & 31, h = lane >> 5;
   for (int mt = 0; mt < MT; mt++) {
@@ -218,25 +273,30 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
     for (int fi = 0; fi < 2; fi++) {
       const int f = 2 * wave + fi;
       const int8_t* pb = y1 + f * y1s + 1024 * mt + 32 * n + 16 * h;
+      // plain float form: the chain starts from the floor form's magic (+ offset >> 3)
+      const int ci = (!rb && !XR) ? k.thr[fi] : 0;
       v16i acc;
 #pragma unroll
-      for (int i = 0; i < 16; i++) acc[i] = 0;
+      for (int i = 0; i < 16; i++) acc[i] = ci;
 #pragma unroll
       for (int s = 0; s < 3; s++)
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[fi][s], *(const v4i*)(pb + 32 * s), acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(k.af[fi][s], *(const v4i*)(pb + 32 * s), acc, 0, 0, 0);
       int q[2];
 #pragma unroll
       for (int w = 0; w < 2; w++) {
         int sum = 0;
         if (rb) {
 #pragma unroll
-          for (int i = 0; i < 8; i++) sum += max(acc[8 * w + i], thr[fi]);
-          q[w] = clampq(xdiv(sum + off[fi], m[fi], xs[fi]), lo);
+          for (int i = 0; i < 8; i++) sum += max(acc[8 * w + i], k.thr[fi]);
+          sum += k.off[fi];
+          q[w] = XR ? clampq(xdiv(sum, k.m[fi], k.xs[fi]), LO) : clampq((int)((float)sum * k.r[fi]), LO);
         } else {
           // func_xcorr_scale per element (clip to int8), ReLU, sum of 8 >> 3
 #pragma unroll
-          for (int i = 0; i < 8; i++) sum += min(max(xdiv(acc[8 * w + i] + off[fi], m[fi], xs[fi]), 0), 127);
-          q[w] = clampq(sum >> 3, lo);
+          for (int i = 0; i < 8; i++)
+            sum += XR ? min(max(xdiv(acc[8 * w + i] + k.off[fi], k.m[fi], k.xs[fi]), 0), 127)
+                      : floor_el<127>(acc[8 * w + i], k.r[fi], k.c[fi]);
+          q[w] = sum >> 3;  // in [0, 127]
         }
       }
       const int u0 = 128 * mt + 4 * n + 2 * h;
@@ -250,11 +310,14 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
 // Layer 3 (layer3.c:49-79, conv.c:105): output u of filter f = sum_j y2p[u + j] W3t[j], y2p[i] at
 // row byte i + 1; four outputs u0 .. u0 + 3 per item from row bytes u0 .. u0 + 19.  Written to
 // y3t[u][f] (net_layer3_flip_inplace as index math).
+template <bool XR, bool CB>
 __device__ __forceinline__ void layer3(const GenParams* __restrict__ gp, const int8_t* y2, int y2s, int8_t* y3,
                                        const SmallG* sg, int wave, int lane) {
-  const int T8 = gp->T8, lo = gp->lo;
+  constexpr int LO = CB ? -127 : -128;
+  const int T8 = gp->T8;
   const unsigned m = gp->l3_m;
   const int xs = gp->l3_xs;
+  const float r = gp->l3_r, c = gp->l3_c;
   const int G = (T8 + 3) >> 2;
   for (int it = lane; it < 2 * G; it += 64) {
     const int fi = it >= G, u0 = 4 * (it - fi * G), f = 2 * wave + fi;
@@ -264,19 +327,22 @@ __device__ __forceinline__ void layer3(const GenParams* __restrict__ gp, const i
     for (int i = 0; i < 5; i++) d[i] = row[i];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      int acc = 0;
+      int acc = XR ? 0 : FMAGIC_I;  // float form: |conv| < 2^22 rides on the magic (exact)
 #pragma unroll
       for (int i = 0; i < 5; i++) acc = __builtin_amdgcn_sdot4(d[i], sg->l3_w[f][k][i], acc, false);
-      if (u0 + k < T8) y3[16 * (u0 + k) + f] = (int8_t)clampq(xdiv(acc, m, xs), lo);
+      const int y = XR ? xdiv(acc, m, xs) : (int)__builtin_fmaf(__int_as_float(acc), r, c);
+      if (u0 + k < T8) y3[16 * (u0 + k) + f] = (int8_t)clampq(y, LO);
     }
   }
 }
 
 // Layer 4 (layer4.c:51-149, FLIP_LAYERS): item (k, v): b = W4[k] . y3t[u] for u = 8 v .. 8 v + 7,
 // REORDER_BN: sum max(b, thr) + off, / fac; plain: sum max(tdiv(b + off >> 3, fac >> 3), 0) >> 3.
+template <bool XR, bool CB>
 __device__ __forceinline__ void layer4(const GenParams* __restrict__ gp, const int8_t* y3, int8_t* y4,
                                        const SmallG* sg, int tid) {
-  const int T64 = gp->T64, T64A = gp->T64A, lo = gp->lo;
+  constexpr int LO = CB ? -127 : -128;
+  const int T64 = gp->T64, T64A = gp->T64A;
   const bool rb = gp->rb != 0;
   for (int it = tid; it < F2 * T64; it += NT) {
     const int k = it & 15, v = it >> 4;
@@ -290,53 +356,56 @@ __device__ __forceinline__ void layer4(const GenParams* __restrict__ gp, const i
       int b = 0;
 #pragma unroll
       for (int q = 0; q < 4; q++) b = __builtin_amdgcn_sdot4(a[q], w[q], b, false);
-      sum += rb ? max(b, thr) : max(xdiv(b + off, m, xs), 0);
+      // plain: layer4.c:113-118 clips no element (the float form clamps at 1024, past which the
+      // result saturates anyway)
+      sum += rb ? max(b, thr) : XR ? max(xdiv(b + off, m, xs), 0) : floor_el<1024>(b + sg->l4_ci[k], sg->l4_r[k], sg->l4_c[k]);
     }
-    y4[k * T64A + v] = (int8_t)clampq(rb ? xdiv(sum + off, m, xs) : sum >> 3, lo);
+    int y;
+    if (!rb) y = sum >> 3;
+    else if (XR) y = xdiv(sum + off, m, xs);
+    else y = (int)((float)(sum + off) * sg->l4_r[k]);
+    y4[k * T64A + v] = (int8_t)clampq(y, LO);
   }
 }
 
 // Layer 5 (layer5.c:43-89, transform.c:47): class n on wave n mod NW; z = W5[n] . y4 + b5[n],
 // clip(z / fac) (pad columns meet zero weights).
+template <bool CB>
 __device__ __forceinline__ void layer5(const GenParams* __restrict__ gp, const int8_t* y4, int8_t* out, int wave,
                                        int lane) {
-  const int N = gp->N, nd = 4 * gp->T64A, lo = gp->lo;  // dwords of y4
+  constexpr int LO = CB ? -127 : -128;
+  const int N = gp->N, nd = 4 * gp->T64A;  // dwords of y4
   for (int n = wave; n < N; n += NW) {
     const int* w = (const int*)gp->l5_w[n];
     int part = 0;
     for (int d = lane; d < nd; d += 64) part = __builtin_amdgcn_sdot4(((const int*)y4)[d], w[d], part, false);
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
-    if (lane == 0) out[n] = (int8_t)clampq(xdiv(part + gp->l5_b[n], gp->l5_m, gp->l5_xs), lo);
+    if (lane == 0) out[n] = (int8_t)clampq(xdiv(part + gp->l5_b[n], gp->l5_m, gp->l5_xs), LO);
   }
 }
 
 // Per-lane constants and the LDS initialisation shared by both kernels.
-struct Lane {
-  v4i wf;             // layer-1 B operand
-  int off1, xs1;
-  unsigned m1;
-  v4i af[2][3];       // layer-2 bands of the wave's two filters
-  int thr2[2], off2[2], xs2[2];
-  unsigned m2[2];
-};
-
-__device__ __forceinline__ void setup(const GenParams* __restrict__ gp, int8_t* smem, const Carve& cv, Lane& R,
-                                      int tid, int wave, int lane) {
+__device__ __forceinline__ void setup(const GenParams* __restrict__ gp, int8_t* smem, const Carve& cv, L1C& k1,
+                                      L2C& k2, int tid, int wave, int lane) {
   const int j = lane & 15;
-  R.wf = gp->l1_b[lane];
-  R.off1 = gp->l1_off[j];
-  R.m1 = gp->l1_m[j];
-  R.xs1 = gp->l1_xs[j];
+  k1.wf = gp->l1_b[lane];
+  k1.off = gp->l1_off[j];
+  k1.m = gp->l1_m[j];
+  k1.xs = gp->l1_xs[j];
+  k1.r = gp->l1_r[j];
+  k1.c = gp->l1_c[j];
 #pragma unroll
   for (int fi = 0; fi < 2; fi++) {
     const int f = 2 * wave + fi;
 #pragma unroll
-    for (int s = 0; s < 3; s++) R.af[fi][s] = gp->l2_a[f][s][lane];
-    R.thr2[fi] = gp->l2_thr[f];
-    R.off2[fi] = gp->l2_off[f];
-    R.m2[fi] = gp->l2_m[f];
-    R.xs2[fi] = gp->l2_xs[f];
+    for (int s = 0; s < 3; s++) k2.af[fi][s] = gp->l2_a[f][s][lane];
+    k2.thr[fi] = gp->l2_thr[f];
+    k2.off[fi] = gp->l2_off[f];
+    k2.m[fi] = gp->l2_m[f];
+    k2.xs[fi] = gp->l2_xs[f];
+    k2.r[fi] = gp->l2_r[f];
+    k2.c[fi] = gp->l2_c[f];
   }
   // zero pads of every row (positions past the data are never rewritten), then the small params
   v4i* z = (v4i*)smem;
@@ -347,7 +416,7 @@ __device__ __forceinline__ void setup(const GenParams* __restrict__ gp, int8_t* 
 }
 
 // Fused forward over a batch of B trials (layout L), logits [B][N].
-template <int L>
+template <int L, bool XR, bool CB>
 __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp, const int8_t* __restrict__ x,
                                                  int8_t* __restrict__ out, int B, float qs, float qy) {
   extern __shared__ v4i smem_v[];
@@ -355,8 +424,9 @@ __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Carve cv = carve_of(gp->T8, gp->T64A, gp->NB1, gp->MT, L != TM);
-  Lane R;
-  setup(gp, smem, cv, R, tid, wave, lane);
+  L1C k1;
+  L2C k2;
+  setup(gp, smem, cv, k1, k2, tid, wave, lane);
   const SmallG* sg = (const SmallG*)(smem + cv.sg);
   int8_t* y1 = smem;
   int8_t* y2 = smem + cv.y2;
@@ -370,21 +440,22 @@ __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp
   // before B; its layers 2-3 come after the next A, which every wave reaches only after C.
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const View v = trial_view<L>(x, b, C, T, xstride);
-    layer1<L>(gp, v, y1, cv.y1s, stg, R.wf, R.off1, R.m1, R.xs1, wave, lane, qs, qy);
+    layer1<L, XR, CB>(gp, v, y1, cv.y1s, stg, k1, wave, lane, qs, qy);
     __syncthreads();  // A
-    layer2(gp, y1, cv.y1s, y2, cv.y2s, R.af, R.thr2, R.off2, R.m2, R.xs2, wave, lane);
+    layer2<XR, CB>(gp, y1, cv.y1s, y2, cv.y2s, k2, wave, lane);
     wg::wave_sync_lds();  // layer 3 of filter f reads only y2 row f, written by this wave
-    layer3(gp, y2, cv.y2s, y3, sg, wave, lane);
+    layer3<XR, CB>(gp, y2, cv.y2s, y3, sg, wave, lane);
     __syncthreads();  // B
-    layer4(gp, y3, y4, sg, tid);
+    layer4<XR, CB>(gp, y3, y4, sg, tid);
     __syncthreads();  // C
-    layer5(gp, y4, out + (size_t)b * N, wave, lane);
+    layer5<CB>(gp, y4, out + (size_t)b * N, wave, lane);
   }
 }
 
 // Single-trial, single-layer kernel for the reference's per-layer entry points on the general
 // path: stage 1..5 = net_layerN, 6 = net_layer3_flip_inplace; reference layouts in and out (pads
 // zero).  Stage 1 takes the trial packed time-major [T][C] (the batched layout).
+template <bool XR, bool CB>
 __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, const int8_t* __restrict__ in,
                                               int8_t* __restrict__ out, int stage) {
   extern __shared__ v4i smem_v[];
@@ -392,8 +463,9 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const Carve cv = carve_of(gp->T8, gp->T64A, gp->NB1, gp->MT, false);
-  Lane R;
-  setup(gp, smem, cv, R, tid, wave, lane);
+  L1C k1;
+  L2C k2;
+  setup(gp, smem, cv, k1, k2, tid, wave, lane);
   const SmallG* sg = (const SmallG*)(smem + cv.sg);
   int8_t* y1 = smem;
   int8_t* y2 = smem + cv.y2;
@@ -404,7 +476,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   __syncthreads();
   if (stage == 1) {  // [T][C] packed -> [F1][T_ALIGN]
     const View v = trial_view<TM>(in, 0, C, T, gp->xstride);
-    layer1<TM>(gp, v, y1, cv.y1s, nullptr, R.wf, R.off1, R.m1, R.xs1, wave, lane, 0.0f, 0.0f);
+    layer1<TM, XR, CB>(gp, v, y1, cv.y1s, nullptr, k1, wave, lane, 0.0f, 0.0f);
     __syncthreads();
     for (int i = tid; i < F2 * TA; i += NT) {
       const int f = i / TA, t = i - f * TA;
@@ -416,7 +488,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
       y1[f * cv.y1s + 32 + t] = in[f * TA + t];
     }
     __syncthreads();
-    layer2(gp, y1, cv.y1s, y2, cv.y2s, R.af, R.thr2, R.off2, R.m2, R.xs2, wave, lane);
+    layer2<XR, CB>(gp, y1, cv.y1s, y2, cv.y2s, k2, wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T8A; i += NT) {
       const int f = i / T8A, u = i - f * T8A;
@@ -428,7 +500,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
       y2[f * cv.y2s + 8 + u] = in[f * T8A + u];
     }
     __syncthreads();
-    layer3(gp, y2, cv.y2s, y3, sg, wave, lane);
+    layer3<XR, CB>(gp, y2, cv.y2s, y3, sg, wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T8A; i += NT) {
       const int f = i / T8A, u = i - f * T8A;
@@ -437,13 +509,13 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   } else if (stage == 4) {  // [T8][F2] -> [F2][T64_ALIGN]
     for (int i = tid; i < T8 * F2; i += NT) y3[i] = in[i];
     __syncthreads();
-    layer4(gp, y3, y4, sg, tid);
+    layer4<XR, CB>(gp, y3, y4, sg, tid);
     __syncthreads();
     for (int i = tid; i < F2 * T64A; i += NT) out[i] = y4[i];
   } else if (stage == 5) {  // [F2][T64_ALIGN] -> [N] (the pad columns read as zero)
     for (int i = tid; i < F2 * T64A; i += NT) y4[i] = (i % T64A) < T64 ? in[i] : 0;
     __syncthreads();
-    layer5(gp, y4, out, wave, lane);
+    layer5<CB>(gp, y4, out, wave, lane);
   } else if (stage == 6) {  // flip [F2][T8_ALIGN] -> [T8][F2]
     for (int i = tid; i < F2 * T8A; i += NT) {
       const int u = i / F2, f = i - u * F2;

@@ -332,6 +332,22 @@ struct Reader {
   }
 };
 
+// The reference multiplies the weight pads too (func_dotp over all C_ALIGN / F2 * T64_ALIGN bytes,
+// layer1.c:90, layer5.c:81) and gen_net_header.py writes them as zeros; the GPU skips them, so a
+// set with non-zero pads is rejected (NET_ERR_BLOB), as ParamSet.validate does.
+int check_pads(const HostParams& hp) {
+  const Dims& d = hp.d;
+  const int F2 = d.F2;
+  for (int f = 0; f < F2; f++)
+    for (int c = d.C; c < d.C_ALIGN(); c++)
+      if (hp.l1_weight_align[(size_t)f * d.C_ALIGN() + c] != 0) return NET_ERR_BLOB;
+  for (int n = 0; n < d.N; n++)
+    for (int k = 0; k < F2; k++)
+      for (int v = d.T64(); v < d.T64_ALIGN(); v++)
+        if (hp.l5_weight[((size_t)n * F2 + k) * d.T64_ALIGN() + v] != 0) return NET_ERR_BLOB;
+  return NET_OK;
+}
+
 int parse_blob(const void* blob, size_t len, HostParams& hp) {
   if (!blob || len < (size_t)HEADER_SIZE) return NET_ERR_BLOB;
   const uint8_t* b = (const uint8_t*)blob;
@@ -364,17 +380,7 @@ int parse_blob(const void* blob, size_t len, HostParams& hp) {
   hp.l5_bias = r.i8(d.N);
   hp.l5_weight = r.w((size_t)d.N * F2 * d.T64_ALIGN(), d.wbits);
   if (!r.ok || r.pos != len) return NET_ERR_BLOB;
-  // The reference multiplies these pads too (func_dotp over all C_ALIGN / F2 * T64_ALIGN bytes,
-  // layer1.c:90, layer5.c:81) and gen_net_header.py writes them as zeros; the GPU skips them, so
-  // a blob with non-zero pads is rejected, as ParamSet.validate does.
-  for (int f = 0; f < F2; f++)
-    for (int c = d.C; c < d.C_ALIGN(); c++)
-      if (hp.l1_weight_align[(size_t)f * d.C_ALIGN() + c] != 0) return NET_ERR_BLOB;
-  for (int n = 0; n < d.N; n++)
-    for (int k = 0; k < F2; k++)
-      for (int v = d.T64(); v < d.T64_ALIGN(); v++)
-        if (hp.l5_weight[((size_t)n * F2 + k) * d.T64_ALIGN() + v] != 0) return NET_ERR_BLOB;
-  return NET_OK;
+  return check_pads(hp);
 }
 
 // ---- device parameter image --------------------------------------------------------------
@@ -644,8 +650,10 @@ int build_devparams(HostParams& hp, DevParams& dp) {
 
 // ---- general-geometry parameter image (forward_gen.hpp) ------------------------------------
 // Every network gen_net_header.py emits with F1 = F2 = 16: C <= 64, 64 <= T <= gen::TMAX,
-// 1 <= N <= gen::NMAX.  Exact integer division at every requant (xdiv), so the same range checks
-// as the specialised image decide NET_ERR_RANGE and nothing else can fail.
+// 1 <= N <= gen::NMAX.  The same range checks as the specialised image decide NET_ERR_RANGE.
+// Requant: the float forms of the compiled kernels where every layer-1..4 requant has one proven
+// exact (gp.xr = 0), exact integer division (xdiv) at layers 1-4 otherwise (gp.xr = 1); layer 5
+// always divides exactly.
 int build_genparams(HostParams& hp, gen::GenParams& gp) {
   const Dims& d = hp.d;
   if (d.F1 != F2 || d.F2 != F2 || d.D != 1) return NET_ERR_UNSUPPORTED;
@@ -707,6 +715,42 @@ int build_genparams(HostParams& hp, gen::GenParams& gp) {
     }
   }
   l2_bands(hp, 1, gp.l2_a);
+  // float forms (the proofs of build_devparams): xr stays 0 only if every one is proven
+  auto floats = [&]() -> bool {
+    const int64_t A = 128 * 128;
+    if (!choose_reciprocal(hp.l3_factor, &gp.l3_r, &gp.l3_c, 128, 16 * A)) return false;
+    for (int f = 0; f < F2; f++) {
+      const Range e1 = rg.e1[f], s2 = rg.s2[f], s4 = rg.s4[f];
+      if (e1.amax() >= (1 << 22) || !choose_reciprocal(hp.l1_factor[f], &gp.l1_r[f], &gp.l1_c[f], 128, e1.amax()))
+        return false;
+      if (hp.reorder_bn) {
+        if (s2.amax() >= (1 << 24) || !choose_reciprocal(hp.l2_factor[f], &gp.l2_r[f], nullptr, 128, s2.amax()))
+          return false;
+        if (s4.amax() >= (1 << 24) || !choose_reciprocal(hp.l4_factor[f], &gp.sg.l4_r[f], nullptr, 128, s4.amax()))
+          return false;
+      } else {
+        int32_t m2, m4;
+        if (s2.amax() >= (1 << 22) ||
+            !choose_floor_form(hp.l2_factor[f] >> 3, 127, s2.amax(), &m2, &gp.l2_r[f], &gp.l2_c[f]))
+          return false;
+        if (s4.amax() >= (1 << 22) ||
+            !choose_floor_form(hp.l4_factor[f] >> 3, 1024, s4.amax(), &m4, &gp.sg.l4_r[f], &gp.sg.l4_c[f]))
+          return false;
+        gp.l2_thr[f] = m2 + (hp.l2_offset[f] >> 3);  // the layer-2 MFMA C-init
+        gp.sg.l4_ci[f] = m4 + (hp.l4_offset[f] >> 3);
+      }
+    }
+    for (int f = 0; f < F2; f++) gp.l1_off[f] = hp.l1_offset[f] + FMAGIC_I;
+    return true;
+  };
+  gp.xr = floats() ? 0 : 1;
+  if (gp.xr) {  // the half-built float constants are unused by the XR kernels; the C-inits revert
+    for (int f = 0; f < F2; f++) {
+      gp.l1_off[f] = hp.l1_offset[f];
+      gp.l2_thr[f] = -(hp.l2_offset[f] >> 3);
+    }
+  }
+  hp.xr = gp.xr != 0;
   const XDiv x3 = xdiv_consts(hp.l3_factor), x5 = xdiv_consts(hp.l5_factor);
   gp.l3_m = x3.m;
   gp.l3_xs = x3.xs;
@@ -1046,18 +1090,28 @@ int gen_blocks_per_cu(Kern k, int lds) {
   return n;
 }
 
-template <int L>
-int launch_gen_t(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
+template <int L, bool XR, bool CB>
+int launch_gen_q(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
                  hipStream_t st, int32_t* info, float qs) {
   const int lds = gen::carve_of(hg.T8, hg.T64A, hg.NB1, hg.MT, L != gen::TM).bytes;
-  const size_t cap = (size_t)ds.cus * (size_t)gen_blocks_per_cu(gen::k_forward<L>, lds);
+  const size_t cap = (size_t)ds.cus * (size_t)gen_blocks_per_cu(gen::k_forward<L, XR, CB>, lds);
   const int grid = (int)(B < cap ? B : cap);
   if (info) { info[0] = grid; info[1] = gen::NT; info[2] = lds; return NET_OK; }
   if (B == 0) return NET_OK;
   const float qy = qs > 0.0f ? 1.0f / qs : 0.0f;  // RN(1 / scale), as the specialised float kernels
-  hipLaunchKernelGGL(gen::k_forward<L>, dim3(grid), dim3(gen::NT), (size_t)lds, st, (const gen::GenParams*)p, x, y,
-                     (int)B, qs, qy);
+  hipLaunchKernelGGL((gen::k_forward<L, XR, CB>), dim3(grid), dim3(gen::NT), (size_t)lds, st,
+                     (const gen::GenParams*)p, x, y, (int)B, qs, qy);
   return hip_err(hipGetLastError());
+}
+
+template <int L>
+int launch_gen_t(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
+                 hipStream_t st, int32_t* info, float qs) {
+  const bool cb = hg.lo == -127;
+  if (hg.xr) return cb ? launch_gen_q<L, true, true>(ds, hg, p, x, y, B, st, info, qs)
+                       : launch_gen_q<L, true, false>(ds, hg, p, x, y, B, st, info, qs);
+  return cb ? launch_gen_q<L, false, true>(ds, hg, p, x, y, B, st, info, qs)
+            : launch_gen_q<L, false, false>(ds, hg, p, x, y, B, st, info, qs);
 }
 
 // layout: 0 time-major int8, 1 channel-major int8, 2 channel-major float32 (scale qs).  himg: the
@@ -1081,9 +1135,14 @@ int launch_layer(const Variant& v, const void* himg, const void* p, const int8_t
   if (v.general()) {
     const gen::GenParams& hg = *(const gen::GenParams*)himg;
     const int lds = gen::carve_of(hg.T8, hg.T64A, hg.NB1, hg.MT, false).bytes;
-    (void)gen_blocks_per_cu(gen::k_layer, lds);  // the LDS attribute
-    hipLaunchKernelGGL(gen::k_layer, dim3(1), dim3(gen::NT), (size_t)lds, st, (const gen::GenParams*)p, in, out, stage);
-    return hip_err(hipGetLastError());
+    auto go = [&](auto kern) {
+      (void)gen_blocks_per_cu(kern, lds);  // the LDS attribute
+      hipLaunchKernelGGL(kern, dim3(1), dim3(gen::NT), (size_t)lds, st, (const gen::GenParams*)p, in, out, stage);
+      return hip_err(hipGetLastError());
+    };
+    const bool cb = hg.lo == -127;
+    if (hg.xr) return cb ? go(gen::k_layer<true, true>) : go(gen::k_layer<true, false>);
+    return cb ? go(gen::k_layer<false, true>) : go(gen::k_layer<false, false>);
   }
   return dispatch(v, [&](auto k) {
     hipLaunchKernelGGL(wg::k_layer<decltype(k)>, dim3(1), dim3(wg::NTHREADS), 0, st, (const DevParams*)p, in, out, stage);
@@ -1258,16 +1317,54 @@ int net_params_load(const void* blob, size_t len) {
   return install(hp);
 }
 
+int net_params_load_arrays(const net_arrays_t* a) {
+  if (!a) return NET_ERR_INVALID;
+  if (a->flags & ~(FLAG_REORDER_BN | FLAG_CLIP_BALANCED)) return NET_ERR_BLOB;
+  Dims d;
+  d.C = a->C; d.T = a->T; d.F1 = a->F1; d.F2 = a->F2; d.D = a->D; d.N = a->N; d.wbits = 8;
+  // the blob header's checks (parse_blob), then the arrays it would carry
+  if (d.C <= 0 || d.T < 64 || d.F1 <= 0 || d.N <= 0 || d.F2 != d.F1 * d.D) return NET_ERR_BLOB;
+  if ((size_t)d.C * d.T > ((size_t)1 << 30) || d.N > 4096 || d.F2 > 4096) return NET_ERR_UNSUPPORTED;
+  if (!a->l1_factor || !a->l1_offset || !a->l1_weight_align || !a->l2_factor || !a->l2_offset ||
+      !a->l2_weight_reverse || !a->l3_weight || !a->l4_factor || !a->l4_offset || !a->l4_weight || !a->l5_bias ||
+      !a->l5_weight)
+    return NET_ERR_INVALID;
+  auto hp = std::make_shared<HostParams>();
+  hp->d = d;
+  hp->reorder_bn = (a->flags & FLAG_REORDER_BN) != 0;
+  hp->clip_balanced = (a->flags & FLAG_CLIP_BALANCED) != 0;
+  const size_t F2 = (size_t)d.F2;
+  auto i32 = [](const int32_t* p, size_t n) { return std::vector<int32_t>(p, p + n); };
+  auto i8 = [](const int8_t* p, size_t n) { return std::vector<int8_t>(p, p + n); };
+  hp->l1_factor = i32(a->l1_factor, F2);
+  hp->l1_offset = i32(a->l1_offset, F2);
+  hp->l1_weight_align = i8(a->l1_weight_align, F2 * d.C_ALIGN());
+  hp->l2_factor = i32(a->l2_factor, F2);
+  hp->l2_offset = i32(a->l2_offset, F2);
+  hp->l2_weight_reverse = i8(a->l2_weight_reverse, F2 * 64);
+  hp->l3_factor = a->l3_factor;
+  hp->l3_weight = i8(a->l3_weight, F2 * 16);
+  hp->l4_factor = i32(a->l4_factor, F2);
+  hp->l4_offset = i32(a->l4_offset, F2);
+  hp->l4_weight = i8(a->l4_weight, F2 * F2);
+  hp->l5_factor = a->l5_factor;
+  hp->l5_bias = i8(a->l5_bias, (size_t)d.N);
+  hp->l5_weight = i8(a->l5_weight, (size_t)d.N * F2 * d.T64_ALIGN());
+  if (const int rc = check_pads(*hp)) return rc;
+  return install(hp);
+}
+
 int net_params_info(int32_t* info) {
   if (!info) return NET_ERR_INVALID;
   Snapshot s = snapshot();
-  for (int i = 0; i < 4; i++) info[i] = 0;
+  for (int i = 0; i < 5; i++) info[i] = 0;
   if (!s.host) return NET_ERR_NO_PARAMS;
   const HostParams& hp = *s.host;
   info[0] = hp.general ? NET_PATH_GENERAL : hp.xr ? NET_PATH_EXACT : NET_PATH_FLOAT;
-  info[1] = hp.general ? 0 : hp.xr_layer;
+  info[1] = hp.general || !hp.xr ? 0 : hp.xr_layer;
   info[2] = hp.general || !hp.xr ? -1 : hp.xr_filter;
   info[3] = hp.general ? -1 : compiled_shape(hp.d);
+  info[4] = hp.xr ? 1 : 0;
   return NET_OK;
 }
 
@@ -1484,6 +1581,17 @@ int mibminet_test_xdiv_gpu(int32_t d, int64_t e0, int64_t count, int64_t* mismat
 int mibminet_test_pool_consts(int32_t off, int32_t layer, int32_t* thr, int32_t* offm) {
   if (!thr || !offm || (layer != 2 && layer != 4)) return NET_ERR_INVALID;
   pool_consts(off, layer == 2 ? (1 << 20) : (1 << 18), thr, offm);
+  return NET_OK;
+}
+
+int mibminet_test_image_digest(uint64_t* digest) {
+  if (!digest) return NET_ERR_INVALID;
+  Snapshot s = snapshot();
+  if (!s.host) return NET_ERR_NO_PARAMS;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a over the image bytes
+  const uint8_t* p = (const uint8_t*)s.img.data.get();
+  for (size_t i = 0; i < s.img.bytes; i++) h = (h ^ p[i]) * 1099511628211ull;
+  *digest = h;
   return NET_OK;
 }
 

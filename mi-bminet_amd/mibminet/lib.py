@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "net_version", "net_quantize_input_f32", "net_quantize_input_f64", "net_argmax_batch",
     "net_pack_trials_i8", "net_model_compute_batch_multi", "net_model_compute_batch_ct",
     "net_model_compute_batch_multi_ct", "net_launch_info_ct", "net_model_compute_batch_f32",
-    "net_model_compute_batch_ct_sync", "net_params_info",
+    "net_model_compute_batch_ct_sync", "net_params_info", "net_params_load_arrays",
 )
 NET_PATH_FLOAT, NET_PATH_EXACT, NET_PATH_GENERAL = 0, 1, 2
 
@@ -263,10 +263,10 @@ def model_compute_batch_ct_sync(x_ptr: int, y_ptr: int, B: int, device: int = 0)
 def params_info() -> dict:
     """net_params_info: which kernels the loaded set runs ("float", "exact" or "general"), and for
     "exact" the first layer / filter whose requant has no proven float form."""
-    arr = (ctypes.c_int32 * 4)()
+    arr = (ctypes.c_int32 * 5)()
     _check(load().net_params_info(arr), "net_params_info")
     path = {NET_PATH_FLOAT: "float", NET_PATH_EXACT: "exact", NET_PATH_GENERAL: "general"}[arr[0]]
-    return {"path": path, "layer": arr[1], "filter": arr[2], "shape": arr[3]}
+    return {"path": path, "layer": arr[1], "filter": arr[2], "shape": arr[3], "exact_division": bool(arr[4])}
 
 
 def force_general(on: bool) -> None:

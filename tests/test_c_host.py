@@ -63,3 +63,31 @@ def test_c_host_bench(gpu, net_host, tmp_path):
     assert r.returncode == 0, r.stderr
     m = re.search(r"([0-9.e+]+) trials/s", r.stdout)
     assert m and float(m.group(1)) > 1e7, r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["net_b22", "net_g19"])
+def test_c_host_linked_net_h(gpu, tmp_path, name):
+    """The C host linked with a generated net.c (the reference's weight globals, examples/c_host/
+    make_nets.py) loads it through net_params_load_arrays (no blob file) and matches the oracle on
+    net_model_compute, net_model_compute_batch and net_model_compute_batch_ct."""
+    import sys
+    sys.path.insert(0, EX)
+    import make_nets
+
+    subprocess.run(["make", "-s", "-C", EX], check=True)
+    ps = make_nets.param_set(name)
+    d = ps.dims
+    n = 20
+    rng = np.random.default_rng(d.C)
+    x = np.stack([oracle.to_tc_align(rng.integers(-128, 128, size=(d.C, d.T)), d.C_ALIGN) for _ in range(n)])
+    co = oracle.COracle(ps)
+    want = np.stack([co.model(xi) for xi in x])
+    (tmp_path / "x.bin").write_bytes(x.astype(np.int8).tobytes())
+    (tmp_path / "want.bin").write_bytes(want.astype(np.int8).tobytes())
+    exe = os.path.join(EX, "net_host_" + name.split("_")[1])
+    r = subprocess.run([exe, "check", "-", str(tmp_path / "x.bin"), str(tmp_path / "want.bin"), str(n)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "parameters: linked net.c" in r.stdout and "ok" in r.stdout
+    assert f"net_model_compute_batch_ct: 0 of {n} trials differ" in r.stdout

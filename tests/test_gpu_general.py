@@ -70,6 +70,7 @@ def test_channel_selected_few_class(C, N, T, gpu):
     """The verdict's sweep: C in {8, 16, 19, 38} x N in {2, 3, 4} x T in {480, 1125}."""
     ps = ParamSet.synthetic(seed=1000 * C + 10 * N + T, C=C, T=T, N=N)
     _check_all_entries(ps, B=61, seed=C + N + T)
+    assert not lib.params_info()["exact_division"]  # calibrated sets: the proven float requant
 
 
 @pytest.mark.parametrize("C,T,N,kw", [
@@ -94,6 +95,7 @@ def test_extreme_requant_sets(C, T, gpu):
     for rb in (True, False):
         ps = ParamSet.synthetic_extreme(seed=C + T + rb, C=C, T=T, reorder_bn=rb)
         _check_all_entries(ps, B=29, seed=C, layers=True)
+        assert lib.params_info()["exact_division"]
 
 
 def test_float_input_general(gpu):

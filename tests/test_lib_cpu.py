@@ -79,7 +79,7 @@ def test_params_load_rejects():
     ps2 = ParamSet.synthetic(seed=1, C=8, T=512, N=3)
     b2 = ps2.to_blob()
     assert L.net_params_load(b2, len(b2)) == lib.NET_OK
-    assert lib.params_info() == {"path": "general", "layer": 0, "filter": -1, "shape": -1}
+    assert lib.params_info() == {"path": "general", "layer": 0, "filter": -1, "shape": -1, "exact_division": False}
     # outside every kernel (T > 4096, N > 16, F1 != 16) fails loudly
     for kw in (dict(C=8, T=4104), dict(C=8, T=512, N=17), dict(C=8, T=512, F1=8)):
         b = ParamSet.synthetic(seed=1, **kw).to_blob()
@@ -87,14 +87,14 @@ def test_params_load_rejects():
     ps1 = ParamSet.synthetic(seed=1)
     b1 = ps1.to_blob()
     assert L.net_params_load(b1, len(b1)) == lib.NET_OK
-    assert lib.params_info() == {"path": "float", "layer": 0, "filter": -1, "shape": 0}
+    assert lib.params_info() == {"path": "float", "layer": 0, "filter": -1, "shape": 0, "exact_division": False}
     # offsets beyond the float envelope load (exact-division kernels); past int32 they are refused
     ps3 = ParamSet.synthetic(seed=1)
     ps3.l1_offset[0] = 4_500_000
     b3 = ps3.to_blob()
     assert L.net_params_load(b3, len(b3)) == lib.NET_OK and L.mibminet_test_params_xr() == 1
     # the public query names the requant that forced the exact path
-    assert lib.params_info() == {"path": "exact", "layer": 1, "filter": 0, "shape": 0}
+    assert lib.params_info() == {"path": "exact", "layer": 1, "filter": 0, "shape": 0, "exact_division": True}
     ps3.l1_offset[0] = 2 ** 31 - 1
     b3 = ps3.to_blob()
     assert L.net_params_load(b3, len(b3)) == lib.NET_ERR_RANGE
