@@ -9,8 +9,9 @@
 // layout serves every geometry; the three geometries of the reference's own configurations keep
 // their compile-time specialisations (forward_wg.hpp), which this file does not touch.
 //
-// One workgroup of NW = 8 wave64s owns one trial at a time (persistent, grid-strided), with three
-// barriers per trial.  Every intermediate stays in LDS:
+// One workgroup of NW = 8 wave64s owns one trial at a time (persistent, grid-strided), with two
+// barriers per trial: waves 0-6 run layer 1 while wave 7 runs layers 4-5 of the previous trial.
+// Int8 trials arrive in LDS a trial ahead by LDS-DMA.  Every intermediate stays in LDS:
 //   layer1  MFMA i32_16x16x64_i8: A = 16 samples x 64 channel slots, B = the 16 filters' weights
 //           (zero past C), C-init = the offset.  Time-major trials: a lane's 16 bytes of sample
 //           t are t C + 16 g .. +15 of the trial, read as five aligned dwords and realigned by
@@ -66,7 +67,8 @@ static_assert(sizeof(SmallG) % 16 == 0, "SmallG is copied in 16-byte pieces");
 // Device parameter image of the general path (built on the host: mibminet.hip, build_genparams).
 struct GenParams {
   int C, T, N, T8;
-  int T64, T64A, NB1, MT;       // NB1: layer-1 blocks of 16 samples; MT: layer-2 tiles of 1024 outputs
+  int T64, T64A, NB1, MT;       // NB1: layer-1 blocks of 16 samples; MT: full layer-2 tiles of 1024 outputs
+  int NTT, pad2[3];             // layer-2 tail tiles of 256 outputs per filter past the MT full tiles
   int rb, lo, xstride, xr;      // REORDER_BN branches; lower clip bound; time-major trial stride;
                                 // exact division (no proven float form for some requant)
   unsigned l3_m;
@@ -88,27 +90,50 @@ struct GenParams {
   int l5_b[NMAX];
   SmallG sg;
   v4i l2_a[F2][3][64];          // layer-2 A operand (banded weights) per filter, K-step and lane
+  v4i l2t_a[F2][2][64];         // layer-2 tail A operand (16 shifts x 128 K-slots) per filter, K-step, lane
   int8_t l5_w[NMAX][L5W];       // [n][k T64A + v], zero pads
 };
 
-// LDS carve of one workgroup (host and device compute it alike).
+constexpr int LDS_MAX = 160 * 1024;    // LDS per CU
+constexpr int LDS_2WG = LDS_MAX / 2;    // two workgroups per CU at most this much each
+
+// bytes of one layer-5 weight row in LDS: F2 T64A rounded up to 256 (64 dwords: the four reads
+// per pass of layer5's sixteen lanes per class need no bound check; the pads are zero)
+__host__ __device__ constexpr int w5_row(int T64A) { return (F2 * T64A + 255) / 256 * 256; }
+
+// LDS carve of one workgroup (host and device compute it alike).  Int8 trials (time-major and
+// channel-major) are staged whole in LDS ("raw", the trial a grid stride ahead arriving by LDS-DMA
+// during layers 2-5) when that fits in LDS_MAX; otherwise, and for float32 trials, layer 1 loads
+// its fragments from memory.
 struct Carve {
   int y1s, y2s;                 // row strides of y1 (positions t + 32) and y2 (positions u + 8)
-  int y2, y3, y4, sg, stg, bytes;
+  int y2, y3, y4, sg, w5, stg, raw, chunks, bytes;  // raw < 0: not staged; chunks: 1 KB DMA pieces
 };
-__host__ __device__ inline Carve carve_of(int T8, int T64A, int NB1, int MT, bool staging) {
+__host__ __device__ inline Carve carve_of(int C, int T, int N, int T8, int T64A, int NB1, int MT, int NTT,
+                                          int layout) {
   Carve c;
-  // layer 2 reads positions < 1024 MT + 64; layer 1 writes positions < 32 + 16 NB1.  Stride = 16
-  // (mod 256): the sixteen filters' layer-1 dword stores of a block fall on distinct banks
-  const int need = cmax(32 + 16 * NB1, 1024 * MT + 64);
+  // layer 2 reads positions < 1024 MT + 64 (full tiles) and < 1024 MT + 256 NTT + 112 (tail);
+  // layer 1 writes positions < 32 + 16 NB1.  Stride = 16 (mod 256): the sixteen filters' layer-1
+  // dword stores of a block fall on distinct banks
+  const int need = cmax(cmax(32 + 16 * NB1, 1024 * MT + 64), NTT ? 1024 * MT + 256 * NTT + 112 : 0);
   c.y1s = (need + 239) / 256 * 256 + 16;
   c.y2s = align16(T8 + 32);     // 8 pad bytes, T8 outputs, zeros under layer 3's 20-byte windows
   c.y2 = 16 * c.y1s;
   c.y3 = c.y2 + 16 * c.y2s;
-  c.y4 = c.y3 + align16(16 * T8);
-  c.sg = c.y4 + align16(16 * T64A);
-  c.stg = c.sg + (int)sizeof(SmallG);
-  c.bytes = c.stg + (staging ? NW * 1024 : 0);
+  c.y4 = c.y3 + align16(16 * (T8 + 3));       // layer 3 stores rows up to T8 + 2 unconditionally
+  c.sg = c.y4 + w5_row(T64A);                 // y4 padded with zeros to whole 256-byte rows
+  c.w5 = c.sg + (int)sizeof(SmallG);          // layer-5 weights [N][w5_row], then the N biases
+  c.stg = c.w5 + N * w5_row(T64A) + align16(4 * N);  // channel-major transpose staging, 1 KB per wave
+  // layout: 0 time-major, 1 channel-major, 2 float32 (gen::Layout); 3: the single-layer kernel
+  const int base = c.stg + ((layout == 1 || layout == 2) ? NW * 1024 : 0);
+  // the trial's bytes from its dword-aligned base (delta <= 3), in 1 KB pieces, plus the slack the
+  // 20-byte fragment windows read past them (time-major: 16 NB1 samples of C bytes; channel-major:
+  // row C - 1 read 16 NB1 samples in)
+  const int bytes = C * T + 3;
+  c.chunks = (bytes + 1023) / 1024;
+  const int region = align16(cmax(cmax(1024 * c.chunks, 16 * NB1 * C + 96), C * T + 16 * NB1 + 96));
+  c.raw = ((layout == 0 || layout == 1) && base + region <= LDS_MAX) ? base : -1;
+  c.bytes = base + (c.raw >= 0 ? region : 0);
   return c;
 }
 
@@ -151,23 +176,23 @@ __device__ __forceinline__ View trial_view(const int8_t* x, long long b, int C, 
 }
 
 // The A fragment of layer-1 block blk (samples 16 blk .. +15), before staging: time-major, lane
-// (j, g) holds channels 16 g .. +15 of sample 16 blk + j (bytes past the sample's C meet zero
-// weights); channel-major, lane c holds samples 16 blk .. +15 of channel c (0 for c >= C).
+// (j, g) holds channels 16 g .. +15 of sample 16 blk + j; channel-major, lane c holds samples
+// 16 blk .. +15 of channel c.  K-slots past C meet zero weights, so what those lanes read does not
+// matter: the loads are unconditional (no per-lane branch between one block's loads and the next
+// block's), and channel-major rows past C re-read row C - 1.
 template <int L>
 __device__ __forceinline__ v4i l1_fetch(const View& v, int blk, int C, int T, int lane, float qs, float qy) {
   if constexpr (L == TM) {
     const int j = lane & 15, g = lane >> 4;
-    if (16 * g >= C) return (v4i){0, 0, 0, 0};
     return load16u(v.r, v.delta + (16 * blk + j) * C + 16 * g);
   } else if constexpr (L == CT) {
-    if (lane >= C) return (v4i){0, 0, 0, 0};
-    return load16u(v.r, v.delta + lane * T + 16 * blk);
+    return load16u(v.r, v.delta + min(lane, C - 1) * T + 16 * blk);
   } else {
-    if (lane >= C) return (v4i){0, 0, 0, 0};
+    const int c = min(lane, C - 1);
     v4i w;
 #pragma unroll
     for (int m = 0; m < 4; m++) {
-      const v4u f = __builtin_amdgcn_raw_buffer_load_b128(v.r, 4 * (lane * T + 16 * blk) + 16 * m, 0, 0);
+      const v4u f = __builtin_amdgcn_raw_buffer_load_b128(v.r, 4 * (c * T + 16 * blk) + 16 * m, 0, 0);
       // the reference's input quantisation (gen_input_header.py:66-76), wg::quantize1_f; the
       // truncating convert lies in [-127, 127]
       int q[4];
@@ -182,6 +207,38 @@ __device__ __forceinline__ v4i l1_fetch(const View& v, int blk, int C, int T, in
 struct TrK {
   static constexpr bool TR16 = false;  // wg::stage_block's P == 1 transpose (ds_read_b64_tr_b8)
 };
+
+// 16 bytes at byte offset o of the staged trial: a 4-byte-aligned ds_read_b128 and the next dword,
+// realigned by v_alignbyte
+__device__ __forceinline__ v4i lds16u(const int8_t* raw, int o) {
+  const int o4 = o & ~3;
+  const unsigned s = (unsigned)(o & 3);
+  const v4u a = *(const v4u*)(raw + o4);
+  const unsigned e = *(const unsigned*)(raw + o4 + 16);
+  return (v4i){(int)__builtin_amdgcn_alignbyte(a[1], a[0], s), (int)__builtin_amdgcn_alignbyte(a[2], a[1], s),
+               (int)__builtin_amdgcn_alignbyte(a[3], a[2], s), (int)__builtin_amdgcn_alignbyte(e, a[3], s)};
+}
+
+// the A fragment of layer-1 block blk from the staged trial (raw: the trial's dword-aligned base;
+// delta: its first byte)
+template <int L>
+__device__ __forceinline__ v4i l1_fetch_lds(const int8_t* raw, int delta, int blk, int C, int T, int lane) {
+  if constexpr (L == TM) {
+    const int j = lane & 15, g = lane >> 4;
+    return lds16u(raw, delta + (16 * blk + j) * C + 16 * g);
+  } else {
+    return lds16u(raw, delta + min(lane, C - 1) * T + 16 * blk);
+  }
+}
+
+// LDS-DMA of trial view v into the raw area: 1 KB pieces i = wave, wave + NW, ... (lane L's 16
+// bytes land at byte 16 L of its piece); pieces past num_records land as zeros.  wg::dma_b128 is
+// inline asm, so no barrier waits for it: the wave waits vmcnt(0) before barrier B (k_forward).
+__device__ __forceinline__ void stage_trial(const View& v, int8_t* raw, int chunks, int wave, int lane) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of the area have returned
+  const unsigned base = wg::lds_addr(raw);
+  for (int i = wave; i < chunks; i += NW) wg::dma_b128(v.r, 1024 * i + 16 * lane, 0, base + 1024 * i);
+}
 
 // Layer 1: this wave's blocks blk = wave, wave + NW, ... -> y1 rows (position 32 + t).  Loads of
 // U blocks are issued before their MFMAs.
@@ -208,22 +265,26 @@ struct L1C {  // a lane's layer-1 constants (filter lane & 15)
   float r, c;
 };
 
-template <int L, bool XR, bool CB>
-__device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const View& v, int8_t* y1, int y1s,
-                                       int8_t* stg, const L1C& k, int wave, int lane, float qs, float qy) {
+// ST: the trial is staged in LDS (sraw).  The U blocks' loads are all issued before the first MFMA
+// (slots past NB1 re-read the last block; their results are not stored).
+template <int L, bool ST, bool XR, bool CB>
+__device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const View& v, const int8_t* sraw, int8_t* y1,
+                                       int y1s, int8_t* stg, const L1C& k, int wave, int lane, float qs, float qy,
+                                       int nw) {
   const int C = gp->C, T = gp->T, NB1 = gp->NB1;
   const int j = lane & 15, g = lane >> 4;
   constexpr int U = L == F32 ? 2 : 4;
-  for (int b0 = wave; b0 < NB1; b0 += U * NW) {
+  for (int b0 = wave; b0 < NB1; b0 += U * nw) {  // the blocks wave, wave + nw, ... (nw waves in layer 1)
     v4i raw[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int blk = b0 + u * NW;
-      raw[u] = blk < NB1 ? l1_fetch<L>(v, blk, C, T, lane, qs, qy) : (v4i){0, 0, 0, 0};
+      const int blk = min(b0 + u * nw, NB1 - 1);
+      if constexpr (ST) raw[u] = l1_fetch_lds<L>(sraw, v.delta, blk, C, T, lane);
+      else raw[u] = l1_fetch<L>(v, blk, C, T, lane, qs, qy);
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const int blk = b0 + u * NW;
+      const int blk = b0 + u * nw;
       if (blk < NB1) {  // wave-uniform
         const v4i a = L == TM ? raw[u] : wg::stage_block<TrK>(raw[u], stg, lane);
         const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, k.wf, (v4i){k.off, k.off, k.off, k.off}, 0, 0, 0);
@@ -247,6 +308,7 @@ __device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const V
 // u0 = 128 mt + 4 n + 2 h and u0 + 1.
 struct L2C {  // a wave's layer-2 constants (filters 2 wave, 2 wave + 1)
   v4i af[2][3];
+  v4i at[2][2];   // tail bands
   int thr[2], off[2], xs[2];
   unsigned m[2];
   float r[2], c[2];
@@ -269,18 +331,23 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
   const bool rb = gp->rb != 0;
   const int n = lane & 31, h = lane >> 5;
   for (int mt = 0; mt < MT; mt++) {
+    // both filters' B slices first: the six LDS reads overlap instead of each MFMA waiting on one
+    v4i bs[2][3];
+#pragma unroll
+    for (int fi = 0; fi < 2; fi++)
+#pragma unroll
+      for (int s = 0; s < 3; s++)
+        bs[fi][s] = *(const v4i*)(y1 + (2 * wave + fi) * y1s + 1024 * mt + 32 * n + 16 * h + 32 * s);
 #pragma unroll
     for (int fi = 0; fi < 2; fi++) {
       const int f = 2 * wave + fi;
-      const int8_t* pb = y1 + f * y1s + 1024 * mt + 32 * n + 16 * h;
       // plain float form: the chain starts from the floor form's magic (+ offset >> 3)
       const int ci = (!rb && !XR) ? k.thr[fi] : 0;
       v16i acc;
 #pragma unroll
       for (int i = 0; i < 16; i++) acc[i] = ci;
 #pragma unroll
-      for (int s = 0; s < 3; s++)
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(k.af[fi][s], *(const v4i*)(pb + 32 * s), acc, 0, 0, 0);
+      for (int s = 0; s < 3; s++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(k.af[fi][s], bs[fi][s], acc, 0, 0, 0);
       int q[2];
 #pragma unroll
       for (int w = 0; w < 2; w++) {
@@ -305,6 +372,44 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
       else if (u0 < T8) *dst = (int8_t)q[0];
     }
   }
+  // Tail: the column blocks past the full tiles, when at most 16 per filter are left (gp->NTT
+  // tiles): MFMA i32_16x16x64_i8, 16 output shifts x 16 columns of 16 outputs, K = the 128
+  // window positions from the column's first output (the band reaches 79 of them).  Lane (col, g)
+  // holds shifts 4 g .. 4 g + 3 of its column: half a pool window, whose other half sits in row
+  // g ^ 1 and arrives by v_permlane16_swap.
+  const int NTT = gp->NTT;
+  const int col = lane & 15, g = lane >> 4;
+  for (int tt = 0; tt < NTT; tt++) {
+    const int p0 = 1024 * MT + 256 * tt + 16 * col;  // the column's first output (row position p0 + 32 - 32)
+    v4i bt[2][2];
+#pragma unroll
+    for (int fi = 0; fi < 2; fi++)
+#pragma unroll
+      for (int s = 0; s < 2; s++) bt[fi][s] = *(const v4i*)(y1 + (2 * wave + fi) * y1s + p0 + 64 * s + 16 * g);
+#pragma unroll
+    for (int fi = 0; fi < 2; fi++) {
+      const int ci = (!rb && !XR) ? k.thr[fi] : 0;
+      v4i acc = (v4i){ci, ci, ci, ci};
+#pragma unroll
+      for (int s = 0; s < 2; s++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(k.at[fi][s], bt[fi][s], acc, 0, 0, 0);
+      int part = 0;
+      if (rb) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) part += max(acc[i], k.thr[fi]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          part += XR ? min(max(xdiv(acc[i] + k.off[fi], k.m[fi], k.xs[fi]), 0), 127) : floor_el<127>(acc[i], k.r[fi], k.c[fi]);
+      }
+      const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)part, (unsigned)part, false, false);
+      const int tot = (int)(sw[0] + sw[1]);  // the whole window (rows g and g ^ 1 hold the same)
+      int q;
+      if (rb) q = XR ? clampq(xdiv(tot + k.off[fi], k.m[fi], k.xs[fi]), LO) : clampq((int)((float)(tot + k.off[fi]) * k.r[fi]), LO);
+      else q = tot >> 3;
+      const int u = (p0 >> 3) + (g >> 1);
+      if (!(g & 1) && u < T8) y2[(2 * wave + fi) * y2s + 8 + u] = (int8_t)q;
+    }
+  }
 }
 
 // Layer 3 (layer3.c:49-79, conv.c:105): output u of filter f = sum_j y2p[u + j] W3t[j], y2p[i] at
@@ -312,26 +417,30 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
 // y3t[u][f] (net_layer3_flip_inplace as index math).
 template <bool XR, bool CB>
 __device__ __forceinline__ void layer3(const GenParams* __restrict__ gp, const int8_t* y2, int y2s, int8_t* y3,
-                                       const SmallG* sg, int wave, int lane) {
+                                       int wave, int lane) {
   constexpr int LO = CB ? -127 : -128;
   const int T8 = gp->T8;
   const unsigned m = gp->l3_m;
   const int xs = gp->l3_xs;
   const float r = gp->l3_r, c = gp->l3_c;
-  const int G = (T8 + 3) >> 2;
-  for (int it = lane; it < 2 * G; it += 64) {
-    const int fi = it >= G, u0 = 4 * (it - fi * G), f = 2 * wave + fi;
-    const int* row = (const int*)(y2 + f * y2s + u0);
-    int d[5];
 #pragma unroll
-    for (int i = 0; i < 5; i++) d[i] = row[i];
+  for (int fi = 0; fi < 2; fi++) {
+    const int f = 2 * wave + fi;  // wave-uniform: the taps come by scalar loads
+    const int* w = &gp->sg.l3_w[f][0][0];
+    for (int u0 = 4 * lane; u0 < T8; u0 += 256) {
+      const int* row = (const int*)(y2 + f * y2s + u0);
+      int d[5];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      int acc = XR ? 0 : FMAGIC_I;  // float form: |conv| < 2^22 rides on the magic (exact)
+      for (int i = 0; i < 5; i++) d[i] = row[i];
+      // no branch inside: outputs past T8 land in rows T8 .. T8 + 2, which nothing reads
 #pragma unroll
-      for (int i = 0; i < 5; i++) acc = __builtin_amdgcn_sdot4(d[i], sg->l3_w[f][k][i], acc, false);
-      const int y = XR ? xdiv(acc, m, xs) : (int)__builtin_fmaf(__int_as_float(acc), r, c);
-      if (u0 + k < T8) y3[16 * (u0 + k) + f] = (int8_t)clampq(y, LO);
+      for (int k = 0; k < 4; k++) {
+        int acc = XR ? 0 : FMAGIC_I;  // float form: |conv| < 2^22 rides on the magic (exact)
+#pragma unroll
+        for (int i = 0; i < 5; i++) acc = __builtin_amdgcn_sdot4(d[i], w[8 * k + i], acc, false);
+        const int y = XR ? xdiv(acc, m, xs) : (int)__builtin_fmaf(__int_as_float(acc), r, c);
+        y3[16 * (u0 + k) + f] = (int8_t)clampq(y, LO);
+      }
     }
   }
 }
@@ -340,48 +449,70 @@ __device__ __forceinline__ void layer3(const GenParams* __restrict__ gp, const i
 // REORDER_BN: sum max(b, thr) + off, / fac; plain: sum max(tdiv(b + off >> 3, fac >> 3), 0) >> 3.
 template <bool XR, bool CB>
 __device__ __forceinline__ void layer4(const GenParams* __restrict__ gp, const int8_t* y3, int8_t* y4,
-                                       const SmallG* sg, int tid) {
+                                       const SmallG* sg, int tid, int nthreads) {
   constexpr int LO = CB ? -127 : -128;
   const int T64 = gp->T64, T64A = gp->T64A;
   const bool rb = gp->rb != 0;
-  for (int it = tid; it < F2 * T64; it += NT) {
-    const int k = it & 15, v = it >> 4;
-    const v4i w = *(const v4i*)sg->l4_w[k];
-    const int thr = sg->l4_thr[k], off = sg->l4_off[k], xs = sg->l4_xs[k];
-    const unsigned m = sg->l4_m[k];
-    int sum = 0;
+  // output channel k = tid & 15 is the same for every item of this thread (nthreads % 16 == 0): its
+  // constants are read once, all before the first item
+  const int k = tid & 15;
+  const v4i w = *(const v4i*)sg->l4_w[k];
+  const int thr = sg->l4_thr[k], off = sg->l4_off[k], xs = sg->l4_xs[k];
+  const unsigned m = sg->l4_m[k];
+  const float r4 = sg->l4_r[k], c4 = sg->l4_c[k];
+  const int ci4 = sg->l4_ci[k];
+  for (int it = tid; it < F2 * T64; it += nthreads) {  // items tid, tid + nthreads, ...
+    const int v = it >> 4;
+    // the eight rows' reads and dot products first (no branch between them), then the branch
+    int b[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const v4i a = *(const v4i*)(y3 + 16 * (8 * v + i));
-      int b = 0;
+      b[i] = 0;
 #pragma unroll
-      for (int q = 0; q < 4; q++) b = __builtin_amdgcn_sdot4(a[q], w[q], b, false);
+      for (int q = 0; q < 4; q++) b[i] = __builtin_amdgcn_sdot4(a[q], w[q], b[i], false);
+    }
+    int sum = 0, y;
+    if (rb) {
+#pragma unroll
+      for (int i = 0; i < 8; i++) sum += max(b[i], thr);
+      y = XR ? xdiv(sum + off, m, xs) : (int)((float)(sum + off) * r4);
+    } else {
       // plain: layer4.c:113-118 clips no element (the float form clamps at 1024, past which the
       // result saturates anyway)
-      sum += rb ? max(b, thr) : XR ? max(xdiv(b + off, m, xs), 0) : floor_el<1024>(b + sg->l4_ci[k], sg->l4_r[k], sg->l4_c[k]);
+#pragma unroll
+      for (int i = 0; i < 8; i++) sum += XR ? max(xdiv(b[i] + off, m, xs), 0) : floor_el<1024>(b[i] + ci4, r4, c4);
+      y = sum >> 3;
     }
-    int y;
-    if (!rb) y = sum >> 3;
-    else if (XR) y = xdiv(sum + off, m, xs);
-    else y = (int)((float)(sum + off) * sg->l4_r[k]);
     y4[k * T64A + v] = (int8_t)clampq(y, LO);
   }
 }
 
-// Layer 5 (layer5.c:43-89, transform.c:47): class n on wave n mod NW; z = W5[n] . y4 + b5[n],
-// clip(z / fac) (pad columns meet zero weights).
+// Layer 5 (layer5.c:43-89, transform.c:47): z = W5[n] . y4 + b5[n], clip(z / fac) (pad columns
+// meet zero weights).  Four classes per wave pass, sixteen lanes each: lane (n, c) sums dwords
+// c, c + 16, ... of its class, a DPP row_shr prefix sum leaves the class total in the row's lane
+// 15.  Class groups g0, g0 + gstep, ... of four classes.
 template <bool CB>
-__device__ __forceinline__ void layer5(const GenParams* __restrict__ gp, const int8_t* y4, int8_t* out, int wave,
-                                       int lane) {
+__device__ __forceinline__ void layer5(const GenParams* __restrict__ gp, const int8_t* y4, const int8_t* w5,
+                                       int8_t* out, int g0, int gstep, int lane) {
   constexpr int LO = CB ? -127 : -128;
-  const int N = gp->N, nd = 4 * gp->T64A;  // dwords of y4
-  for (int n = wave; n < N; n += NW) {
-    const int* w = (const int*)gp->l5_w[n];
+  const int N = gp->N, rp = w5_row(gp->T64A) / 4;  // dwords of a padded y4 / weight row
+  const int c = lane & 15;
+  const int* b5 = (const int*)(w5 + N * 4 * rp);
+  for (int n0 = 4 * g0; n0 < N; n0 += 4 * gstep) {
+    const int n = n0 + (lane >> 4);
+    const int* w = (const int*)(w5 + (n < N ? n : 0) * 4 * rp);
     int part = 0;
-    for (int d = lane; d < nd; d += 64) part = __builtin_amdgcn_sdot4(((const int*)y4)[d], w[d], part, false);
+    for (int d = c; d < rp; d += 64) {  // rp is a multiple of 64: four independent reads per pass
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) part += __shfl_xor(part, o, 64);
-    if (lane == 0) out[n] = (int8_t)clampq(xdiv(part + gp->l5_b[n], gp->l5_m, gp->l5_xs), LO);
+      for (int q = 0; q < 4; q++)
+        part = __builtin_amdgcn_sdot4(((const int*)y4)[d + 16 * q], w[d + 16 * q], part, false);
+    }
+    part += __builtin_amdgcn_update_dpp(0, part, 0x111, 0xF, 0xF, true);  // row_shr:1
+    part += __builtin_amdgcn_update_dpp(0, part, 0x112, 0xF, 0xF, true);  // row_shr:2
+    part += __builtin_amdgcn_update_dpp(0, part, 0x114, 0xF, 0xF, true);  // row_shr:4
+    part += __builtin_amdgcn_update_dpp(0, part, 0x118, 0xF, 0xF, true);  // row_shr:8
+    if (c == 15 && n < N) out[n] = (int8_t)clampq(xdiv(part + b5[n], gp->l5_m, gp->l5_xs), LO);
   }
 }
 
@@ -400,6 +531,8 @@ __device__ __forceinline__ void setup(const GenParams* __restrict__ gp, int8_t* 
     const int f = 2 * wave + fi;
 #pragma unroll
     for (int s = 0; s < 3; s++) k2.af[fi][s] = gp->l2_a[f][s][lane];
+#pragma unroll
+    for (int s = 0; s < 2; s++) k2.at[fi][s] = gp->l2t_a[f][s][lane];
     k2.thr[fi] = gp->l2_thr[f];
     k2.off[fi] = gp->l2_off[f];
     k2.m[fi] = gp->l2_m[f];
@@ -413,17 +546,26 @@ __device__ __forceinline__ void setup(const GenParams* __restrict__ gp, int8_t* 
   const v4i* src = (const v4i*)&gp->sg;
   v4i* dst = (v4i*)(smem + cv.sg);
   for (int i = tid; i < (int)(sizeof(SmallG) / 16); i += NT) dst[i] = src[i];
+  const int row5 = F2 * gp->T64A, rp = w5_row(gp->T64A) / 4;  // layer-5 weight rows, [N][rp dwords]
+  int* w5 = (int*)(smem + cv.w5);
+  for (int i = tid; i < gp->N * rp; i += NT) {
+    const int n = i / rp, d = i - n * rp;
+    w5[i] = 4 * d < row5 ? ((const int*)gp->l5_w[n])[d] : 0;
+  }
+  for (int n = tid; n < gp->N; n += NT) w5[gp->N * rp + n] = gp->l5_b[n];
 }
 
 // Fused forward over a batch of B trials (layout L), logits [B][N].
-template <int L, bool XR, bool CB>
+// ST: int8 trials staged in LDS (the carve's raw area fits; the host picks the instantiation)
+template <int L, bool ST, bool XR, bool CB>
 __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp, const int8_t* __restrict__ x,
                                                  int8_t* __restrict__ out, int B, float qs, float qy) {
+  static_assert(!ST || L != F32, "float32 trials are not staged");
   extern __shared__ v4i smem_v[];
   int8_t* smem = (int8_t*)smem_v;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const Carve cv = carve_of(gp->T8, gp->T64A, gp->NB1, gp->MT, L != TM);
+  const Carve cv = carve_of(gp->C, gp->T, gp->N, gp->T8, gp->T64A, gp->NB1, gp->MT, gp->NTT, L);
   L1C k1;
   L2C k2;
   setup(gp, smem, cv, k1, k2, tid, wave, lane);
@@ -434,22 +576,62 @@ __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp
   int8_t* y4 = smem + cv.y4;
   int8_t* stg = smem + cv.stg + 1024 * wave;
   const int C = gp->C, T = gp->T, N = gp->N, xstride = gp->xstride;
+  // int8 trials staged in LDS (cv.raw >= 0, uniform): the first one now; after that each trial a
+  // grid stride ahead, by LDS-DMA issued after barrier A (layer 1 has read the area) and waited for
+  // before barrier B, so it lands during layers 2-3 and no wave waits on HBM in layer 1
+  int8_t* sraw = ST ? smem + cv.raw : nullptr;
+  if (ST && (int)blockIdx.x < B) {
+    stage_trial(trial_view<L>(x, blockIdx.x, C, T, xstride), sraw, cv.chunks, wave, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
-  // Barriers per trial: A (layer 2 reads every wave's layer-1 rows), B (layer 4 reads every
-  // filter), C (layer 5 reads all of y4).  The next trial's layer 1 writes only y1, last read
-  // before B; its layers 2-3 come after the next A, which every wave reaches only after C.
+  // (phase stamps in tools/ builds with -DMIB_STAMPS: 0 layer 1 / the last wave's layers 4-5,
+  // 1 barrier A, 2 layer 2, 3 layer 3, 4 barrier B, 7 loop top)
+  MIB_STAMP_INIT
+  // Two barriers per trial.  Waves 0 .. NW-2 run layer 1 while the last wave runs layers 4 and 5
+  // of the previous trial (its y3t and y4 are untouched until this trial's layer 3, after barrier
+  // A), as the compiled kernels do (forward_wg.hpp); A: layer 2 reads every wave's layer-1 rows;
+  // B: layer 4 reads every filter's layer-3 rows.  The next trial's LDS-DMA goes out after A (layer
+  // 1 has read the area) and is waited for before B.
+  int bprev = -1;
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const View v = trial_view<L>(x, b, C, T, xstride);
-    layer1<L, XR, CB>(gp, v, y1, cv.y1s, stg, k1, wave, lane, qs, qy);
+    MIB_STAMP(7)
+    // priorities as in the compiled kernels (wg::PRIO_*): the last wave's layers 4-5 are the longest
+    // dependency chain of the interval and issue first; layer 1 ahead of the other workgroup's 2-3
+    if (wave < NW - 1) {
+      __builtin_amdgcn_s_setprio(wg::PRIO_L1);
+      layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, wave, lane, qs, qy, NW - 1);
+    } else if (bprev >= 0) {
+      __builtin_amdgcn_s_setprio(wg::PRIO_L45);
+      layer4<XR, CB>(gp, y3, y4, sg, lane, 64);
+      wg::wave_sync_lds();
+      layer5<CB>(gp, y4, smem + cv.w5, out + (size_t)bprev * N, 0, 1, lane);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    MIB_STAMP(0)
     __syncthreads();  // A
+    const int bn = b + (int)gridDim.x;
+    if (ST && bn < B) stage_trial(trial_view<L>(x, bn, C, T, xstride), sraw, cv.chunks, wave, lane);
+    MIB_STAMP(1)
     layer2<XR, CB>(gp, y1, cv.y1s, y2, cv.y2s, k2, wave, lane);
     wg::wave_sync_lds();  // layer 3 of filter f reads only y2 row f, written by this wave
-    layer3<XR, CB>(gp, y2, cv.y2s, y3, sg, wave, lane);
+    MIB_STAMP(2)
+    __builtin_amdgcn_s_setprio(wg::PRIO_L3);
+    layer3<XR, CB>(gp, y2, cv.y2s, y3, wave, lane);
+    __builtin_amdgcn_s_setprio(0);
+    MIB_STAMP(3)
+    if (ST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of the next trial
     __syncthreads();  // B
-    layer4<XR, CB>(gp, y3, y4, sg, tid);
-    __syncthreads();  // C
-    layer5<CB>(gp, y4, out + (size_t)b * N, wave, lane);
+    MIB_STAMP(4)
+    bprev = b;
   }
+  if (wave == NW - 1 && bprev >= 0) {  // the last trial's layers 4-5
+    layer4<XR, CB>(gp, y3, y4, sg, lane, 64);
+    wg::wave_sync_lds();
+    layer5<CB>(gp, y4, smem + cv.w5, out + (size_t)bprev * N, 0, 1, lane);
+  }
+  MIB_STAMP_FLUSH(lane == 0, wave)
 }
 
 // Single-trial, single-layer kernel for the reference's per-layer entry points on the general
@@ -462,7 +644,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   int8_t* smem = (int8_t*)smem_v;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const Carve cv = carve_of(gp->T8, gp->T64A, gp->NB1, gp->MT, false);
+  const Carve cv = carve_of(gp->C, gp->T, gp->N, gp->T8, gp->T64A, gp->NB1, gp->MT, gp->NTT, 3);
   L1C k1;
   L2C k2;
   setup(gp, smem, cv, k1, k2, tid, wave, lane);
@@ -476,7 +658,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   __syncthreads();
   if (stage == 1) {  // [T][C] packed -> [F1][T_ALIGN]
     const View v = trial_view<TM>(in, 0, C, T, gp->xstride);
-    layer1<TM, XR, CB>(gp, v, y1, cv.y1s, nullptr, k1, wave, lane, 0.0f, 0.0f);
+    layer1<TM, false, XR, CB>(gp, v, nullptr, y1, cv.y1s, nullptr, k1, wave, lane, 0.0f, 0.0f, NW);
     __syncthreads();
     for (int i = tid; i < F2 * TA; i += NT) {
       const int f = i / TA, t = i - f * TA;
@@ -500,7 +682,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
       y2[f * cv.y2s + 8 + u] = in[f * T8A + u];
     }
     __syncthreads();
-    layer3<XR, CB>(gp, y2, cv.y2s, y3, sg, wave, lane);
+    layer3<XR, CB>(gp, y2, cv.y2s, y3, wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T8A; i += NT) {
       const int f = i / T8A, u = i - f * T8A;
@@ -509,13 +691,13 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   } else if (stage == 4) {  // [T8][F2] -> [F2][T64_ALIGN]
     for (int i = tid; i < T8 * F2; i += NT) y3[i] = in[i];
     __syncthreads();
-    layer4<XR, CB>(gp, y3, y4, sg, tid);
+    layer4<XR, CB>(gp, y3, y4, sg, tid, NT);
     __syncthreads();
     for (int i = tid; i < F2 * T64A; i += NT) out[i] = y4[i];
   } else if (stage == 5) {  // [F2][T64_ALIGN] -> [N] (the pad columns read as zero)
     for (int i = tid; i < F2 * T64A; i += NT) y4[i] = (i % T64A) < T64 ? in[i] : 0;
     __syncthreads();
-    layer5<CB>(gp, y4, out, wave, lane);
+    layer5<CB>(gp, y4, smem + cv.w5, out, wave, NW, lane);  // class group w on wave w
   } else if (stage == 6) {  // flip [F2][T8_ALIGN] -> [T8][F2]
     for (int i = tid; i < F2 * T8A; i += NT) {
       const int u = i / F2, f = i - u * F2;

@@ -670,7 +670,11 @@ int build_genparams(HostParams& hp, gen::GenParams& gp) {
   gp.T64A = T64A;
   gp.NB1 = (d.T + 15) / 16;
   const int NB2 = (8 * T8 + 31) / 32;  // layer-2 column blocks of 32 outputs
-  gp.MT = (NB2 + 31) / 32;
+  // full 32x32 tiles of 32 blocks; at most 16 blocks left go to 16x16x64 tail tiles (16 columns of
+  // 16 outputs each), more to one more full tile
+  const int rest = NB2 % 32;
+  gp.MT = NB2 / 32 + (rest > 16 ? 1 : 0);
+  gp.NTT = (rest > 0 && rest <= 16) ? (2 * rest + 15) / 16 : 0;
   gp.rb = hp.reorder_bn ? 1 : 0;
   gp.lo = hp.clip_balanced ? -127 : -128;
   gp.xstride = (int)(((size_t)C * d.T + 15) / 16 * 16);
@@ -715,6 +719,19 @@ int build_genparams(HostParams& hp, gen::GenParams& gp) {
     }
   }
   l2_bands(hp, 1, gp.l2_a);
+  // tail bands (gen::layer2): lane (shift m = lane & 15, g) of K-step s holds K-slots
+  // 64 s + 16 g .. +15, window position k of the column meets tap k - m - 1
+  for (int f = 0; f < F2; f++)
+    for (int s = 0; s < 2; s++)
+      for (int lane = 0; lane < 64; lane++) {
+        const int m = lane & 15, g = lane >> 4;
+        int8_t bytes[16];
+        for (int jj = 0; jj < 16; jj++) {
+          const int idx = 64 * s + 16 * g + jj - m - 1;
+          bytes[jj] = (idx >= 0 && idx < 64) ? hp.l2_weight_reverse[(size_t)f * 64 + idx] : 0;
+        }
+        std::memcpy(&gp.l2t_a[f][s][lane], bytes, 16);
+      }
   // float forms (the proofs of build_devparams): xr stays 0 only if every one is proven
   auto floats = [&]() -> bool {
     const int64_t A = 128 * 128;
@@ -1090,28 +1107,39 @@ int gen_blocks_per_cu(Kern k, int lds) {
   return n;
 }
 
-template <int L, bool XR, bool CB>
+template <int L, bool ST, bool XR, bool CB>
 int launch_gen_q(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
                  hipStream_t st, int32_t* info, float qs) {
-  const int lds = gen::carve_of(hg.T8, hg.T64A, hg.NB1, hg.MT, L != gen::TM).bytes;
-  const size_t cap = (size_t)ds.cus * (size_t)gen_blocks_per_cu(gen::k_forward<L, XR, CB>, lds);
+  const int lds = gen::carve_of(hg.C, hg.T, hg.N, hg.T8, hg.T64A, hg.NB1, hg.MT, hg.NTT, L).bytes;
+  const size_t cap = (size_t)ds.cus * (size_t)gen_blocks_per_cu(gen::k_forward<L, ST, XR, CB>, lds);
   const int grid = (int)(B < cap ? B : cap);
   if (info) { info[0] = grid; info[1] = gen::NT; info[2] = lds; return NET_OK; }
   if (B == 0) return NET_OK;
   const float qy = qs > 0.0f ? 1.0f / qs : 0.0f;  // RN(1 / scale), as the specialised float kernels
-  hipLaunchKernelGGL((gen::k_forward<L, XR, CB>), dim3(grid), dim3(gen::NT), (size_t)lds, st,
+  hipLaunchKernelGGL((gen::k_forward<L, ST, XR, CB>), dim3(grid), dim3(gen::NT), (size_t)lds, st,
                      (const gen::GenParams*)p, x, y, (int)B, qs, qy);
   return hip_err(hipGetLastError());
 }
 
+template <int L, bool ST>
+int launch_gen_s(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
+                 hipStream_t st, int32_t* info, float qs) {
+  const bool cb = hg.lo == -127;
+  if (hg.xr) return cb ? launch_gen_q<L, ST, true, true>(ds, hg, p, x, y, B, st, info, qs)
+                       : launch_gen_q<L, ST, true, false>(ds, hg, p, x, y, B, st, info, qs);
+  return cb ? launch_gen_q<L, ST, false, true>(ds, hg, p, x, y, B, st, info, qs)
+            : launch_gen_q<L, ST, false, false>(ds, hg, p, x, y, B, st, info, qs);
+}
+
+// int8 trials that fit in LDS run the staged instantiation (gen::carve_of)
 template <int L>
 int launch_gen_t(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
                  hipStream_t st, int32_t* info, float qs) {
-  const bool cb = hg.lo == -127;
-  if (hg.xr) return cb ? launch_gen_q<L, true, true>(ds, hg, p, x, y, B, st, info, qs)
-                       : launch_gen_q<L, true, false>(ds, hg, p, x, y, B, st, info, qs);
-  return cb ? launch_gen_q<L, false, true>(ds, hg, p, x, y, B, st, info, qs)
-            : launch_gen_q<L, false, false>(ds, hg, p, x, y, B, st, info, qs);
+  if constexpr (L != gen::F32) {
+    if (gen::carve_of(hg.C, hg.T, hg.N, hg.T8, hg.T64A, hg.NB1, hg.MT, hg.NTT, L).raw >= 0)
+      return launch_gen_s<L, true>(ds, hg, p, x, y, B, st, info, qs);
+  }
+  return launch_gen_s<L, false>(ds, hg, p, x, y, B, st, info, qs);
 }
 
 // layout: 0 time-major int8, 1 channel-major int8, 2 channel-major float32 (scale qs).  himg: the
@@ -1134,7 +1162,7 @@ int launch_layer(const Variant& v, const void* himg, const void* p, const int8_t
                  hipStream_t st) {
   if (v.general()) {
     const gen::GenParams& hg = *(const gen::GenParams*)himg;
-    const int lds = gen::carve_of(hg.T8, hg.T64A, hg.NB1, hg.MT, false).bytes;
+    const int lds = gen::carve_of(hg.C, hg.T, hg.N, hg.T8, hg.T64A, hg.NB1, hg.MT, hg.NTT, 3).bytes;
     auto go = [&](auto kern) {
       (void)gen_blocks_per_cu(kern, lds);  // the LDS attribute
       hipLaunchKernelGGL(kern, dim3(1), dim3(gen::NT), (size_t)lds, st, (const gen::GenParams*)p, in, out, stage);

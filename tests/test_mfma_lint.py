@@ -84,14 +84,30 @@ def test_lint_finds_hazards_across_branches(tmp_path):
     assert 24 not in whys and 23 not in whys             # 5 wait states after a 4-pass MFMA: outside the WAR window
     assert has(38, "RAW, window 8")    # asm reads a 4-pass MFMA's result 4 states after it
     assert has(41, "RAW, needs 2")     # MFMA reads an asm output with no wait state between
-    assert len(found) == 6
+    assert has(38, "asm first reader")  # ... and no compiler-emitted instruction read it first
+    assert len(found) == 7
 
 
 def test_no_inline_asm_hazard_next_to_mfma(device_asm):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "mfma_lint.py"), str(device_asm)],
                        check=True, capture_output=True, text=True)
-    hazards = [l for l in r.stdout.splitlines() if "asm write into" in l]
+    hazards = [l for l in r.stdout.splitlines() if "asm write into" in l or "asm first reader" in l]
     assert not hazards, "\n".join(hazards)
+
+
+def test_lint_flags_the_round5_clamp_form():
+    """Round 5's clamp-bit layer-2 form (a) returned wrong logits on the GPU at random; form (b),
+    the same arithmetic with a compiler-emitted first reader of the accumulator, was exact
+    (DESIGN.md §3).  The lint's asm-first-reader rule flags the failing build's device code (an
+    excerpt committed as a fixture) on all eight accumulator pairs and nothing in form (b); the
+    shipped build stays clean (test_no_inline_asm_hazard_next_to_mfma)."""
+    golden = os.path.join(ROOT, "tests", "golden")
+    with open(os.devnull, "w") as null:
+        bad = mfma_lint.lint(os.path.join(golden, "r05_clamp_form_a.s"), out=null)
+        good = mfma_lint.lint(os.path.join(golden, "r05_clamp_form_b.s"), out=null)
+    first = sorted(line for (line, why) in bad if "asm first reader" in why)
+    assert len(first) == 8, bad
+    assert not good, good
 
 
 @pytest.fixture(scope="module")

@@ -19,6 +19,15 @@
   MFMA read of asm output    an MFMA reads as srcA/srcB/srcC a register an inline-asm instruction
                              wrote fewer than 2 wait states earlier (VALU write -> MFMA operand
                              read needs 2; hipcc pads one state after ;;#ASMEND)
+  asm first reader           an inline-asm instruction reads a register of an MFMA's destination
+                             before any compiler-emitted instruction has read or overwritten it, at
+                             any distance.  Round 5's clamp-bit layer-2 form did this (v_pk_fma_f32
+                             ... clamp on the 32x32x32 accumulator, 12 or 24 wait states after the
+                             MFMA, the compiler's own count before its readers) and returned wrong
+                             logits on 1-3 of 300 trials, different ones every run, while the same
+                             arithmetic with a compiler-emitted first reader was exact (DESIGN.md
+                             §3, "The clamp-form wrong logits").  The shipped kernels never let
+                             inline asm read an accumulator first.
 
 Why inline asm: the compiler's hazard recognizer inserts the required wait states (s_nop) for every
 instruction it emitted itself, but it cannot see into inline asm, so neither the WAR nor the WAW
@@ -155,16 +164,22 @@ def walk_mfma(ins, labels, m, report):
     window = PASSES.get(mf.op, DEFAULT_PASSES)
     n = len(ins)
     seen = set()
-    stack = [(k, 0, frozenset(mf.dst), 0) for k in successors(ins, m, labels, n)]
+    # pend: destination registers nothing has read or overwritten yet; fresh: those no
+    # compiler-emitted instruction has read or overwritten yet
+    stack = [(k, 0, frozenset(mf.dst), frozenset(mf.dst), 0) for k in successors(ins, m, labels, n)]
     while stack:
-        k, ws, pend, depth = stack.pop()
+        k, ws, pend, fresh, depth = stack.pop()
         if k is None or k >= n or depth > 400:
             continue
-        key = (k, min(ws, window), pend)
+        key = (k, min(ws, window), pend, fresh)
         if key in seen:
             continue
         seen.add(key)
         it = ins[k]
+        if it.asm and it.src & fresh:
+            report(it, f"asm first reader of the result of the MFMA at line {mf.line} ({ws} wait states; no "
+                       "compiler-emitted reader before it)")
+        fresh = fresh - it.dst if it.asm else fresh - it.src - it.dst
         if it.asm and ws < window and it.dst & src_c:
             report(it, f"asm write into srcC of the MFMA at line {mf.line} after {ws} wait state(s) (WAR, window {window})")
         if it.asm and ws < raw_window(window) and it.src & pend:
@@ -175,10 +190,10 @@ def walk_mfma(ins, labels, m, report):
                 report(it, f"asm write into pending dst of the MFMA at line {mf.line}")
             pend = pend - it.dst
         ws2 = ws + it.wait_states()
-        if ws2 >= raw_window(window) and not pend:
+        if ws2 >= raw_window(window) and not pend and not fresh:
             continue
         for s in successors(ins, k, labels, n):
-            stack.append((s, ws2, pend, depth + 1))
+            stack.append((s, ws2, pend, fresh, depth + 1))
 
 
 def asm_before_mfma(ins, m, report):

@@ -12,6 +12,7 @@ int main(int argc, char** argv) {
   std::ifstream f(argv[1], std::ios::binary);
   std::vector<char> blob((std::istreambuf_iterator<char>(f)), {});
   int8_t *x, *y;
+  if (getenv("MIB_FORCE_GENERAL")) mibminet_test_force_general(1);  // the run-time-dimension kernels
   int rc = net_params_load(blob.data(), blob.size());
   if (rc) { printf("load rc %d\n", rc); return 1; }
   size_t B = argc > 2 ? atol(argv[2]) : 65536;
@@ -25,7 +26,7 @@ int main(int argc, char** argv) {
     if (f32) return net_model_compute_batch_f32((const float*)x, y, B, 3.0f, 0, nullptr);
     return ct ? net_model_compute_batch_ct(x, y, B, 0, nullptr) : net_model_compute_batch_async(x, y, B, 0, nullptr);
   };
-  hipMalloc(&x, B * stride); hipMalloc(&y, B * 4);
+  hipMalloc(&x, B * stride); hipMalloc(&y, B * 16);
   std::vector<int8_t> hx(B * stride);
   for (size_t i = 0; i < hx.size(); i++) hx[i] = (int8_t)(rand() & 255);
   if (f32)  // floats in about [-4, 4]: exponent 0x40 / 0xC0 high byte, random mantissa
