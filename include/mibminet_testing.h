@@ -74,6 +74,10 @@ int mibminet_test_force_general(int on);
  * equal digests mean the two loads produce the same kernels' inputs. */
 int mibminet_test_image_digest(uint64_t* digest);
 
+/* Number of constant filters the loaded set had folded (zero weights, offset +-y, factor +-1) to
+ * stay on the float requant kernels: 0 unless the set as given needed exact division. */
+int mibminet_test_folded_filters(int32_t* count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace mib {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -197,7 +199,9 @@ __device__ __forceinline__ unsigned sat8x4_b(int a, int b, int c, int d) {
 struct L1Tile {
   v4i wf;
   int ci;
-  float rr, cc;
+  float rr, cc;      // float requant: reciprocal and magic constant
+  unsigned xm;       // XR: xdiv magic and shift word, carried as integers (never in a float)
+  int xs;
 };
 
 // Two requant fmas / multiplies on float bit patterns, issued as two v_fma_f32 / v_mul_f32: packed

@@ -358,7 +358,8 @@ struct Regs {
   __device__ __forceinline__ L1Tile& tile(int t) { return t == 0 ? t0 : t1; }
   v4i af[FPW][3];          // layer-2 band fragments of the wave's filters
   int thr2[FPW], off2[FPW];  // REORDER_BN: biased threshold, offset + 8 thr; plain: MFMA C-init, magic c bits
-  float r2[FPW];             // reciprocal (XR: bits of the xdiv magic)
+  float r2[FPW];             // reciprocal
+  unsigned m2[FPW];          // XR: xdiv magic
   int xs2[FPW];              // XR: xdiv shift word
   v4i a31, a32;            // layer-3 tile-1 / tile-2 band fragments of the wave's filter pair
   float r3, c3;            // layer-3 requant constants (uniform)
@@ -674,8 +675,13 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
     R.xoff = lane_xoff<K>(lane, wave);
     T.wf = K::CT ? prm->l1_wfrag_ct[t][lane] : prm->l1_wfrag[t][lane];
     T.ci = prm->l1_cinit[t][lane & 15];
-    T.rr = prm->l1_r[t][lane & 15];
-    T.cc = prm->l1_c[t][lane & 15];
+    if constexpr (K::XR) {
+      T.xm = prm->l1_m[t][lane & 15];
+      T.xs = prm->l1_xs[t][lane & 15];
+    } else {
+      T.rr = prm->l1_r[t][lane & 15];
+      T.cc = prm->l1_c[t][lane & 15];
+    }
   }
 #pragma unroll
   for (int fi = 0; fi < FPW; fi++) {
@@ -685,11 +691,13 @@ __device__ __forceinline__ void setup(const DevParams* __restrict__ prm, int8_t*
     if constexpr (K::RB) {
       R.thr2[fi] = prm->l2_thrb[f];
       R.off2[fi] = prm->l2_offm[f];
-      R.r2[fi] = prm->l2_r[f];
+      if constexpr (K::XR) R.m2[fi] = prm->l2_m[f];
+      else R.r2[fi] = prm->l2_r[f];
     } else {
       R.thr2[fi] = prm->sp.l2n_ci[f];
       R.off2[fi] = __float_as_int(prm->sp.l2n_c[f]);
-      R.r2[fi] = prm->sp.l2n_r[f];
+      if constexpr (K::XR) R.m2[fi] = prm->sp.l2n_m[f];
+      else R.r2[fi] = prm->sp.l2n_r[f];
     }
     if constexpr (K::XR) R.xs2[fi] = prm->sp.l2_xs[f];
   }
@@ -750,7 +758,7 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
     int y[4];
     if constexpr (K::XR) {  // acc = dot + off (C-init = off): exact division
 #pragma unroll
-      for (int r = 0; r < 4; r++) y[r] = xdiv(acc[r], __float_as_uint(T.rr), __float_as_int(T.cc));
+      for (int r = 0; r < 4; r++) y[r] = xdiv(acc[r], T.xm, T.xs);
     } else {
       // acc bits = 1.5*2^23 + (dot + off) as f32; fma(x, r, -1.5*2^23*r) == RN((dot+off)*r)
       const f2 q01 = fma2(acc[0], acc[1], T.rr, T.cc);
@@ -1094,15 +1102,18 @@ __device__ __forceinline__ int xelem_sum8(const v16i& acc, unsigned m, int xs) {
   return ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
 }
 
-// Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].
+// Pooled + requantised pair of layer-2 outputs of one lane: bytes [y(u0), y(u0+1)].  rm: the
+// reciprocal, or (XR) the xdiv magic.
 template <int LO, bool XR>
-__device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, float r, int xs) {
+__device__ __forceinline__ unsigned l2_out(const v16i& acc, int thr, int off, std::conditional_t<XR, unsigned, float> rm,
+                                           int xs) {
   if constexpr (XR) {
-    const unsigned m = __float_as_uint(r);
-    return sat8x2<LO>(xdiv(pool8b<0>(acc, thr, off), m, xs), xdiv(pool8b<8>(acc, thr, off), m, xs));
+    return sat8x2<LO>(xdiv(pool8b<0>(acc, thr, off), rm, xs), xdiv(pool8b<8>(acc, thr, off), rm, xs));
+  } else {
+    const float r = rm;
+    const f2 q = mul2((float)pool8b<0>(acc, thr, off), (float)pool8b<8>(acc, thr, off), r);
+    return sat8x2<LO>((int)q[0], (int)q[1]);
   }
-  const f2 q = mul2((float)pool8b<0>(acc, thr, off), (float)pool8b<8>(acc, thr, off), r);
-  return sat8x2<LO>((int)q[0], (int)q[1]);
 }
 
 // Layer-2 tail: outputs 1024 MT + 16 bq + m (m < 16) of the wave's two filters, one column of 16
@@ -1184,9 +1195,10 @@ __device__ __forceinline__ void layer2(const int8_t* smem_y1, int8_t* smem_y2, c
       // reg i of this lane = shift 16h + i of block m -> pooled samples u0 (i<8), u0+1 (i>=8)
       unsigned w;
       if constexpr (K::RB) {
-        w = l2_out<K::LO, K::XR>(acc, R.thr2[fi], R.off2[fi], R.r2[fi], K::XR ? R.xs2[fi] : 0);
+        if constexpr (K::XR) w = l2_out<K::LO, true>(acc, R.thr2[fi], R.off2[fi], R.m2[fi], R.xs2[fi]);
+        else w = l2_out<K::LO, false>(acc, R.thr2[fi], R.off2[fi], R.r2[fi], 0);
       } else if constexpr (K::XR) {
-        const unsigned m = __float_as_uint(R.r2[fi]);
+        const unsigned m = R.m2[fi];
         w = (unsigned)(xelem_sum8<0, 127>(acc, m, R.xs2[fi]) >> 3) | ((unsigned)(xelem_sum8<8, 127>(acc, m, R.xs2[fi]) >> 3) << 8);
       } else {
         w = l2n_out(acc, R.r2[fi], __int_as_float(R.off2[fi]));
@@ -1274,8 +1286,8 @@ __device__ __forceinline__ unsigned l4_out(const v16i& acc, const SmallParams* s
 #define MIB_K4(arr, T) (*(const T*)((const char*)(arr) + kb))
   if constexpr (K::RB) {
     const int thrb = MIB_K4(sp->l4_thr, int) + bias, offm = MIB_K4(sp->l4_offm, int);
-    const float r4 = MIB_K4(sp->l4_r, float);
-    return l2_out<K::LO, K::XR>(acc, thrb, offm, r4, K::XR ? MIB_K4(sp->l4_xs, int) : 0);
+    if constexpr (K::XR) return l2_out<K::LO, true>(acc, thrb, offm, MIB_K4(sp->l4_m, unsigned), MIB_K4(sp->l4_xs, int));
+    else return l2_out<K::LO, false>(acc, thrb, offm, MIB_K4(sp->l4_r, float), 0);
   } else if constexpr (K::XR) {
     const unsigned m = MIB_K4(sp->l4n_m, unsigned);
     const int xs = MIB_K4(sp->l4_xs, int);

@@ -70,6 +70,7 @@ struct HostParams {
   bool xr = false;             // set at load: exact integer division at layers 1, 2, 4 (Cfg::XR)
   int xr_layer = 0, xr_filter = -1;  // the first requant without a proven float form (xr = true)
   bool general = false;        // set at load: the run-time-dimension kernels (forward_gen.hpp)
+  int folded = 0;              // set at load: constant filters folded (fold_constant_filters)
 };
 
 // test hook (mibminet_test_force_general): load every later set on the general path
@@ -430,6 +431,76 @@ int check_ranges(const HostParams& hp, Ranges& rg) {
   }
   if (hp.l3_factor == 0 || hp.l5_factor == 0) return NET_ERR_RANGE;
   return NET_OK;
+}
+
+// Per-filter classification ahead of the float / exact choice.  A layer-1, -2 or -4 filter whose
+// output is one value y over its whole reachable numerator range
+// (a rail: an offset far past anything the weights reach, a factor that sends every sum to zero, a
+// REORDER_BN threshold above every conv value) is folded into zero weights with offset y and
+// factor 1, or offset -y and factor -1 when y < 0 (a pooled sum of zeros with offset |y| and
+// threshold -(|y| >> 3) <= 0 is |y|).  The kernels then produce the same y for every input with
+// either requant form, and the filter no longer takes the set off the float kernels.  trunc(v /
+// fac) and the clip are monotone in v, so the output is constant iff it is equal at both ends of
+// the range.  Returns the count.
+int fold_constant_filters(HostParams& h, const Ranges& rg) {
+  const Dims& d = h.d;
+  const int64_t lo = h.clip_balanced ? -127 : -128;
+  auto q = [&](int64_t v, int64_t fac) { return std::min<int64_t>(127, std::max<int64_t>(lo, v / fac)); };
+  auto constant = [&](const Range& r, int32_t fac, int32_t* y) {
+    const int64_t a = q(r.lo, fac), b = q(r.hi, fac);
+    *y = (int32_t)a;
+    return a == b;
+  };
+  int n = 0;
+  const int CA = d.C_ALIGN();
+  for (int f = 0; f < d.F2; f++) {
+    int32_t y;
+    if (constant(rg.e1[f], h.l1_factor[f], &y)) {
+      std::fill_n(&h.l1_weight_align[(size_t)f * CA], CA, (int8_t)0);
+      h.l1_offset[f] = y;
+      h.l1_factor[f] = 1;
+      n++;
+    }
+    if (!h.reorder_bn) {
+      // plain branches: the elements e = trunc((conv + (off >> 3)) / (fac >> 3)) (clipped in layer
+      // 2, not in the C's layer 4) go through max(e, 0), a sum of 8 and // 8 (and the final clip in
+      // layer 4): the output is 0 when every e <= 0, 127 when every e >= 127, e when e is
+      // constant.  Folded: factor 8 and offset 8 y, so every element is y (in [0, 127]).
+      auto plain = [&](const Range& r, int32_t fac, int32_t* yp) {
+        const int64_t a = r.lo / (int64_t)(fac >> 3), b = r.hi / (int64_t)(fac >> 3);
+        const int64_t emin = std::min(a, b), emax = std::max(a, b);
+        if (emax > 0 && emin < 127 && emin != emax) return false;
+        *yp = (int32_t)std::min<int64_t>(127, std::max<int64_t>(0, emin));
+        return true;
+      };
+      if (plain(rg.s2[f], h.l2_factor[f], &y)) {
+        std::fill_n(&h.l2_weight_reverse[(size_t)f * 64], 64, (int8_t)0);
+        h.l2_offset[f] = 8 * y;
+        h.l2_factor[f] = 8;
+        n++;
+      }
+      if (plain(rg.s4[f], h.l4_factor[f], &y)) {
+        std::fill_n(&h.l4_weight[(size_t)f * d.F2], d.F2, (int8_t)0);
+        h.l4_offset[f] = 8 * y;
+        h.l4_factor[f] = 8;
+        n++;
+      }
+      continue;
+    }
+    if (constant(rg.s2[f], h.l2_factor[f], &y)) {
+      std::fill_n(&h.l2_weight_reverse[(size_t)f * 64], 64, (int8_t)0);
+      h.l2_offset[f] = y < 0 ? -y : y;
+      h.l2_factor[f] = y < 0 ? -1 : 1;
+      n++;
+    }
+    if (constant(rg.s4[f], h.l4_factor[f], &y)) {
+      std::fill_n(&h.l4_weight[(size_t)f * d.F2], d.F2, (int8_t)0);
+      h.l4_offset[f] = y < 0 ? -y : y;
+      h.l4_factor[f] = y < 0 ? -1 : 1;
+      n++;
+    }
+  }
+  return n;
 }
 
 // Layer-2 A operand = banded weights (wg::layer2 and gen::layer2): row i <-> shift n(i) so that
@@ -1319,16 +1390,38 @@ namespace {
 // Builds the device image of a parsed set and makes it current: the compiled kernels when its
 // geometry has them, the general kernels otherwise.
 int install(std::shared_ptr<HostParams> hp) {
-  Image img;
   hp->general = g_force_general.load() != 0 || compiled_shape(hp->d) < 0;
-  if (hp->general) {
-    auto gp = std::make_shared<gen::GenParams>();
-    if (const int rc = build_genparams(*hp, *gp)) return rc;
-    img = make_image(gp);
-  } else {
-    auto dp = std::make_shared<DevParams>();
-    if (const int rc = build_devparams(*hp, *dp)) return rc;
-    img = make_image(dp);
+  auto build = [&](HostParams& h, Image* img) -> int {
+    if (h.general) {
+      auto gp = std::make_shared<gen::GenParams>();
+      if (const int rc = build_genparams(h, *gp)) return rc;
+      *img = make_image(gp);
+    } else {
+      auto dp = std::make_shared<DevParams>();
+      if (const int rc = build_devparams(h, *dp)) return rc;
+      *img = make_image(dp);
+    }
+    return NET_OK;
+  };
+  Image img;
+  if (const int rc = build(*hp, &img)) return rc;
+  if (hp->xr) {
+    // off the float envelope: fold the constant filters into an equivalent copy (the reference
+    // ranges, NET_ERR_RANGE included, were checked on the set as given) and keep that image, float
+    // if every remaining requant is proven, exact otherwise (xr_layer / xr_filter then name a
+    // filter that really varies)
+    HostParams fh = *hp;
+    Ranges rg;
+    if (check_ranges(fh, rg) == NET_OK && (fh.folded = fold_constant_filters(fh, rg)) > 0) {
+      Image fimg;
+      if (build(fh, &fimg) == NET_OK) {
+        img = fimg;
+        hp->xr = fh.xr;
+        hp->xr_layer = fh.xr_layer;
+        hp->xr_filter = fh.xr_filter;
+        hp->folded = fh.folded;
+      }
+    }
   }
   std::lock_guard<std::mutex> lk(g_mu);
   g_host = hp;
@@ -1620,6 +1713,14 @@ int mibminet_test_image_digest(uint64_t* digest) {
   const uint8_t* p = (const uint8_t*)s.img.data.get();
   for (size_t i = 0; i < s.img.bytes; i++) h = (h ^ p[i]) * 1099511628211ull;
   *digest = h;
+  return NET_OK;
+}
+
+int mibminet_test_folded_filters(int32_t* count) {
+  if (!count) return NET_ERR_INVALID;
+  Snapshot s = snapshot();
+  if (!s.host) return NET_ERR_NO_PARAMS;
+  *count = s.host->folded;
   return NET_OK;
 }
 

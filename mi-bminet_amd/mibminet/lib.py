@@ -119,6 +119,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     L.net_params_info.restype = i
     # test hooks (include/mibminet_testing.h)
     L.mibminet_test_force_general.argtypes = [i]
+    L.mibminet_test_folded_filters.argtypes = [vp]
+    L.mibminet_test_folded_filters.restype = i
     L.mibminet_test_force_general.restype = i
     L.mibminet_test_xdiv_host.argtypes = [vp, sz, ctypes.c_int32, vp]
     L.mibminet_test_xdiv_host.restype = i
@@ -275,6 +277,13 @@ def force_general(on: bool) -> None:
     _check(load().mibminet_test_force_general(1 if on else 0), "mibminet_test_force_general")
 
 
+def folded_filters() -> int:
+    """Test hook (mibminet_test_folded_filters): constant filters the loaded set had folded."""
+    v = ctypes.c_int32(0)
+    _check(load().mibminet_test_folded_filters(ctypes.byref(v)), "mibminet_test_folded_filters")
+    return v.value
+
+
 def params_exact_division() -> bool:
     """True when the loaded set runs the exact integer-division kernels (Cfg::XR: a set outside the
     float requant envelope), False for the float-requant kernels."""
@@ -406,16 +415,17 @@ def pack_trials_torch(x, stream=None):
     return y
 
 
-def check_trials(x, channel_major: bool) -> None:
+def check_trials(x, channel_major: bool, require_contiguous: bool = True) -> None:
     """Raises ValueError unless ``x`` (NumPy array or torch tensor) is a C-contiguous int8 batch of
     trials in the chosen layout (check_trial_shape).  The C ABI sees only pointers and counts, so a
     batch of another element type (e.g. int64 from rng.integers) or with strides would otherwise
-    run and its bytes be read as int8 trials."""
+    run and its bytes be read as int8 trials.  ``require_contiguous=False``: callers that copy the
+    batch contiguously themselves before it reaches a pointer (shard.forward_devices)."""
     dt = str(getattr(x, "dtype", ""))
     if dt not in ("int8", "torch.int8"):
         raise ValueError(f"trials must be int8, got {dt or type(x).__name__}")
     contiguous = x.is_contiguous() if hasattr(x, "is_contiguous") else bool(x.flags["C_CONTIGUOUS"])
-    if not contiguous:
+    if require_contiguous and not contiguous:
         raise ValueError("trials must be C-contiguous")
     check_trial_shape(tuple(x.shape), channel_major)
 

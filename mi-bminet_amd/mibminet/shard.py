@@ -81,7 +81,9 @@ def forward_devices(x_global, devices, channel_major: bool = False):
     from . import lib
 
     world = len(devices)
-    lib.check_trials(x_global, channel_major)  # before any device work
+    # dtype and shape before any device work; each shard is copied contiguously below, so strided
+    # views are fine here (model_compute_batch_multi checks the contiguous copies)
+    lib.check_trials(x_global, channel_major, require_contiguous=False)
     xs, ys = [], []
     n_out = lib._dims().N
     for r, d in enumerate(devices):

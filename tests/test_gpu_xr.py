@@ -149,3 +149,36 @@ def test_extreme_full_batch(gpu):
     idx = np.concatenate([np.arange(16), B - 16 + np.arange(16), rng.choice(B, 256, replace=False)])
     xs = xp[torch.from_numpy(idx).cuda()].cpu().numpy()
     assert np.array_equal(y.cpu().numpy()[idx], oracle.COracle(ps).batch(xs, nthreads=NT))
+
+
+@pytest.mark.parametrize("C,T,rb,cb", [(22, 1125, True, False), (22, 1125, False, True), (64, 1000, True, True),
+                                       (64, 480, False, False), (19, 480, True, False), (38, 1125, False, False)])
+def test_folded_rail_sets_on_the_float_kernels(C, T, rb, cb, gpu):
+    """Sets whose out-of-envelope filters are all constant load on the float kernels with those
+    filters folded (mibminet.hip, fold_constant_filters); the outputs equal the C oracle on the set
+    as given, batched (both layouts) and through the reference's single-trial and layer entries."""
+    import torch
+
+    ps = ParamSet.synthetic_extreme(61 + C, C=C, T=T, reorder_bn=rb, clip_balanced=cb, mids=0)
+    lib.params_load(ps)
+    assert not lib.params_exact_division() and lib.folded_filters() >= 15
+    rng = np.random.default_rng(C + T)
+    B = 67
+    x = rng.integers(-128, 128, size=(B, C, T)).astype(np.int8)
+    x[-1] = 127
+    x[-2] = -128
+    xp = pack_trials(x)
+    co = oracle.COracle(ps)
+    want = co.batch(xp, nthreads=NT)
+    assert np.array_equal(lib.forward_torch(torch.from_numpy(xp).cuda()).cpu().numpy(), want)
+    assert np.array_equal(lib.forward_ct_torch(torch.from_numpy(x).cuda()).cpu().numpy(), want)
+    d = ps.dims
+    xa = oracle.to_tc_align(x[0], d.C_ALIGN)
+    y1 = co.layer1(xa)
+    np.testing.assert_array_equal(lib.net_layer1(xa), y1)
+    y2 = co.layer2(y1)
+    np.testing.assert_array_equal(lib.net_layer2(y1), y2)
+    y3t = co.layer3_flip(co.layer3(y2))
+    y4 = co.layer4(y3t)
+    np.testing.assert_array_equal(lib.net_layer4(y3t), y4)
+    np.testing.assert_array_equal(lib.net_model_compute(xa), co.model(xa))

@@ -92,6 +92,11 @@ def test_params_load_rejects():
     ps3 = ParamSet.synthetic(seed=1)
     ps3.l1_offset[0] = 4_500_000
     b3 = ps3.to_blob()
+    # ... onto the +127 rail with the calibrated factor: folded, float kernels
+    assert L.net_params_load(b3, len(b3)) == lib.NET_OK and L.mibminet_test_params_xr() == 0
+    assert lib.folded_filters() == 1
+    ps3.l1_factor[0] = 1 << 16  # outputs that still vary: exact division
+    b3 = ps3.to_blob()
     assert L.net_params_load(b3, len(b3)) == lib.NET_OK and L.mibminet_test_params_xr() == 1
     # the public query names the requant that forced the exact path
     assert lib.params_info() == {"path": "exact", "layer": 1, "filter": 0, "shape": 0, "exact_division": True}

@@ -115,3 +115,34 @@ def test_gpu_forward_devices(gpu, devices, B):
     rng = np.random.default_rng(B)
     x = pack_trials(rng.integers(-128, 128, size=(B, 22, 1125)))
     assert np.array_equal(forward_devices(x, devices), oracle.COracle(ps).batch(x, nthreads=8))
+
+
+def test_check_trials_contiguity_flag():
+    """check_trials refuses strided batches at the raw-pointer entries; forward_devices copies
+    every shard contiguously itself and accepts a strided view (dtype and shape still checked)."""
+    from mibminet import lib
+
+    lib.params_load(ParamSet.synthetic(seed=3))
+    x = np.zeros((8, 22, 1125), np.int8)[::2]
+    with pytest.raises(ValueError):
+        lib.check_trials(x, True)
+    lib.check_trials(x, True, require_contiguous=False)
+    with pytest.raises(ValueError):
+        lib.check_trials(x.astype(np.int16), True, require_contiguous=False)
+
+
+@pytest.mark.gpu
+def test_gpu_forward_devices_strided_view(gpu):
+    """A strided view (every other trial of a larger batch) through forward_devices equals the
+    oracle on the same trials."""
+    import oracle
+    from mibminet import lib
+    from mibminet.shard import forward_devices
+
+    ps = ParamSet.synthetic(seed=62)
+    lib.params_load(ps)
+    rng = np.random.default_rng(5)
+    x = rng.integers(-128, 128, size=(300, 22, 1125)).astype(np.int8)
+    view = x[::3]
+    want = oracle.COracle(ps).batch(pack_trials(np.ascontiguousarray(view)), nthreads=8)
+    assert np.array_equal(forward_devices(view, [0, 0], channel_major=True), want)

@@ -82,17 +82,24 @@ def test_layer1_boundaries(f):
             ps.l1_factor[f] = fac
         return _load(ps)
 
-    assert at((1 << 22) - 1 - hi) == (0, False)
-    assert at((1 << 22) - hi) == (0, True)
-    assert at(-(1 << 22) + 1 - lo) == (0, False)
-    assert at(-(1 << 22) - lo) == (0, True)
-    assert at(I32_MAX - hi) == (0, True)
+    # factor 2^15: the outputs still vary near |v| = 2^22 (a rail would be folded, below)
+    F = 1 << 15
+    assert at((1 << 22) - 1 - hi, F) == (0, False)
+    assert at((1 << 22) - hi, F) == (0, True)
+    assert at(-(1 << 22) + 1 - lo, F) == (0, False)
+    assert at(-(1 << 22) - lo, F) == (0, True)
+    # at the int32 ends a factor with the output step 99 -> 100 inside the reachable range
+    Fe = (I32_MAX - (hi - lo) // 2) // 100
+    assert at(I32_MAX - hi, Fe) == (0, True)
     assert at(I32_MAX - hi + 1)[0] == lib.NET_ERR_RANGE
-    assert at(I32_MIN - lo) == (0, True)
+    assert at(I32_MIN - lo, -Fe) == (0, True)
     assert at(I32_MIN - lo - 1)[0] == lib.NET_ERR_RANGE
-    # INT_MIN reachable: / -1 is undefined in C, / -2 is not
+    # INT_MIN reachable: / -1 is undefined in C, / -2 is not (every output then sits on the +127
+    # rail: folded, float kernels)
     assert at(I32_MIN - lo, -1)[0] == lib.NET_ERR_RANGE
-    assert at(I32_MIN - lo, -2) == (0, True)
+    assert at(I32_MIN - lo, -2) == (0, False) and lib.folded_filters() == 1
+    # the calibrated factor with the offset at the int32 end: a rail, folded
+    assert at(I32_MAX - hi) == (0, False) and lib.folded_filters() == 1
 
 
 @pytest.mark.parametrize("name,f", [("l2", 3), ("l4", 9)])
@@ -103,14 +110,18 @@ def test_pooled_boundaries(name, f):
     ps0 = ParamSet.synthetic(seed=4)
     lo, hi = dot_ranges(ps0)[1 if name == "l2" else 2][f]
 
-    def at(off):
+    def at(off, fac=None):
         ps = ParamSet.synthetic(seed=4)
         getattr(ps, f"{name}_offset")[f] = off
+        if fac is not None:
+            getattr(ps, f"{name}_factor")[f] = fac
         return _load(ps)
 
-    assert at((1 << 24) - 1 - 8 * hi) == (0, False)
-    assert at((1 << 24) - 8 * hi) == (0, True)
-    assert at(I32_MAX - 8 * hi) == (0, True)
+    # factors that keep the outputs varying (a rail would be folded onto the float kernels)
+    assert at((1 << 24) - 1 - 8 * hi, 1 << 17) == (0, False)
+    assert at((1 << 24) - 8 * hi, 1 << 17) == (0, True)
+    assert at(I32_MAX - 8 * hi, (I32_MAX - 4 * (hi - lo)) // 100) == (0, True)
+    assert at(I32_MAX - 8 * hi) == (0, False) and lib.folded_filters() == 1
     assert at(I32_MAX - 8 * hi + 1)[0] == lib.NET_ERR_RANGE
     # every element suppressed: sum = 8 thr + off = off & 7, on the float kernels
     assert at(I32_MIN + 8) == (0, False)
@@ -131,7 +142,7 @@ def test_plain_layer4_sum_overflow():
         return _load(ps)
 
     limit = I32_MAX // 8 - hi  # largest off3 with 8 (hi + off3) <= INT32_MAX
-    assert at(limit) == (0, True)
+    assert at(limit) == (0, False) and lib.folded_filters() == 1  # every element >= 127: a rail
     assert at(limit + 1)[0] == lib.NET_ERR_RANGE
 
 
@@ -177,3 +188,99 @@ def test_pool_constants_keep_the_pooled_sum():
                     continue
                 got = (int(np.maximum(v - thr_c.value, 0).sum()) + offm.value) % (1 << 32)
                 assert (got - (1 << 32) if got > I32_MAX else got) == want, (layer, off, v.tolist())
+
+
+def _fold(ps):
+    """Python restatement of the loader's constant-filter folding (mibminet.hip,
+    fold_constant_filters): a filter whose clipped output is one value y over its whole reachable
+    numerator range gets zero weights and offset/factor that reproduce y."""
+    import copy
+
+    q = copy.deepcopy(ps)
+    lo_clip = -127 if ps.clip_balanced else -128
+    r1, r2, r4 = dot_ranges(ps)
+    F2, CA = ps.dims.F2, ps.dims.C_ALIGN
+    w1 = q.l1_weight_align.reshape(F2, CA)
+
+    def out(v, fac):
+        return min(127, max(lo_clip, tdiv(v, fac)))
+
+    n = 0
+    for f in range(F2):
+        off, fac = int(ps.l1_offset[f]), int(ps.l1_factor[f])
+        lo, hi = r1[f]
+        if out(lo + off, fac) == out(hi + off, fac):
+            w1[f] = 0
+            q.l1_offset[f], q.l1_factor[f] = out(lo + off, fac), 1
+            n += 1
+        for name, rr, w in (("l2", r2, q.l2_weight_reverse), ("l4", r4, q.l4_weight)):
+            off, fac = int(getattr(ps, f"{name}_offset")[f]), int(getattr(ps, f"{name}_factor")[f])
+            lo, hi = rr[f]
+            if ps.reorder_bn:
+                thr = -(off >> 3)
+                a, b = out(8 * max(lo, thr) + off, fac), out(8 * max(hi, thr) + off, fac)
+                if a != b:
+                    continue
+                y, o2, f2 = a, abs(a), (-1 if a < 0 else 1)
+            else:
+                e = sorted((tdiv(lo + (off >> 3), fac >> 3), tdiv(hi + (off >> 3), fac >> 3)))
+                if e[1] > 0 and e[0] < 127 and e[0] != e[1]:
+                    continue
+                y = min(127, max(0, e[0]))
+                o2, f2 = 8 * y, 8
+            w[f] = 0
+            getattr(q, f"{name}_offset")[f], getattr(q, f"{name}_factor")[f] = o2, f2
+            n += 1
+    return q, n
+
+
+@pytest.mark.parametrize("rb", [True, False])
+@pytest.mark.parametrize("cb", [False, True])
+def test_constant_filters_fold_onto_the_float_kernels(rb, cb):
+    """Item 6 of round 5's verdict: per-filter classification.  A set whose out-of-envelope filters
+    all sit on a rail (or at zero, or suppressed by the REORDER_BN threshold) loads on the float
+    kernels, the compiled shapes and the general kernels alike; one varying filter past the
+    envelope still takes it to exact division, and params_info names that filter."""
+    for C, T in ((22, 1125), (64, 480), (19, 480)):
+        ps = ParamSet.synthetic_extreme(3 + C, C=C, T=T, reorder_bn=rb, clip_balanced=cb, mids=0)
+        assert _load(ps) == (0, False), (C, T)
+        _, n = _fold(ps)
+        assert lib.folded_filters() == n >= 15
+        ps1 = ParamSet.synthetic_extreme(3 + C, C=C, T=T, reorder_bn=rb, clip_balanced=cb, mids=1)
+        assert _load(ps1) == (0, True), (C, T)
+        info = lib.params_info()
+        if info["path"] == "exact":
+            folded, _ = _fold(ps1)
+            layer, f = info["layer"], info["filter"]
+            # the named filter is not one the loader folded: its parameters are unchanged
+            name = f"l{layer}"
+            assert getattr(folded, f"{name}_factor")[f] == getattr(ps1, f"{name}_factor")[f]
+            assert getattr(folded, f"{name}_offset")[f] == getattr(ps1, f"{name}_offset")[f]
+
+
+@pytest.mark.parametrize("rb", [True, False])
+def test_folding_keeps_the_oracle_outputs(rb):
+    """The folded set computes the original's outputs (C oracle, every layer), on random trials and
+    on the all-rail inputs; the loader folds the same filters."""
+    import oracle
+
+    ps = ParamSet.synthetic_extreme(29, C=22, T=1125, reorder_bn=rb, mids=6)
+    folded, n = _fold(ps)
+    assert n >= 14
+    assert _load(ps)[0] == 0 and lib.folded_filters() == n
+    rng = np.random.default_rng(4)
+    x = rng.integers(-128, 128, size=(24, 22, 1125)).astype(np.int8)
+    x[0], x[1], x[2] = 127, -128, 0
+    from mibminet.params import pack_trials
+    xp = pack_trials(x)
+    a, b = oracle.COracle(ps), oracle.COracle(folded)
+    assert np.array_equal(a.batch(xp, nthreads=4), b.batch(xp, nthreads=4))
+    d = ps.dims
+    for t in range(3):
+        xa = oracle.to_tc_align(x[t], d.C_ALIGN)
+        y1 = a.layer1(xa)
+        assert np.array_equal(y1, b.layer1(xa))
+        y2 = a.layer2(y1)
+        assert np.array_equal(y2, b.layer2(y1))
+        y3t = a.layer3_flip(a.layer3(y2))
+        assert np.array_equal(a.layer4(y3t), b.layer4(y3t))
