@@ -208,27 +208,30 @@ struct TrK {
   static constexpr bool TR16 = false;  // wg::stage_block's P == 1 transpose (ds_read_b64_tr_b8)
 };
 
-// 16 bytes at byte offset o of the staged trial: a 4-byte-aligned ds_read_b128 and the next dword,
-// realigned by v_alignbyte
+// 16 bytes at byte offset o of the staged trial: five aligned dwords, realigned by v_alignbyte.  Not
+// a ds_read_b128 at the 4-byte-aligned address: off its 16-byte alignment that one is replayed at
+// 64 LDS cycles per wave-instruction (MI355X_MICROARCH.md, LDS), which made layer 1 the LDS
+// array's largest user (tools/_adhoc timing proxies, DESIGN.md §3 general kernels)
 __device__ __forceinline__ v4i lds16u(const int8_t* raw, int o) {
   const int o4 = o & ~3;
   const unsigned s = (unsigned)(o & 3);
-  const v4u a = *(const v4u*)(raw + o4);
-  const unsigned e = *(const unsigned*)(raw + o4 + 16);
-  return (v4i){(int)__builtin_amdgcn_alignbyte(a[1], a[0], s), (int)__builtin_amdgcn_alignbyte(a[2], a[1], s),
-               (int)__builtin_amdgcn_alignbyte(a[3], a[2], s), (int)__builtin_amdgcn_alignbyte(e, a[3], s)};
+  const unsigned* p = (const unsigned*)(raw + o4);
+  unsigned d[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) d[i] = p[i];
+  return (v4i){(int)__builtin_amdgcn_alignbyte(d[1], d[0], s), (int)__builtin_amdgcn_alignbyte(d[2], d[1], s),
+               (int)__builtin_amdgcn_alignbyte(d[3], d[2], s), (int)__builtin_amdgcn_alignbyte(d[4], d[3], s)};
 }
 
 // the A fragment of layer-1 block blk from the staged trial (raw: the trial's dword-aligned base;
-// delta: its first byte)
-template <int L>
+// delta: its first byte).  AL: every fragment is 16-byte aligned (delta = 0 and the row length, C
+// time-major or T channel-major, a multiple of 16), one ds_read_b128 each; otherwise lds16u (at
+// C = 64 its five dwords per lane would also meet 8-way bank conflicts).
+template <int L, bool AL>
 __device__ __forceinline__ v4i l1_fetch_lds(const int8_t* raw, int delta, int blk, int C, int T, int lane) {
-  if constexpr (L == TM) {
-    const int j = lane & 15, g = lane >> 4;
-    return lds16u(raw, delta + (16 * blk + j) * C + 16 * g);
-  } else {
-    return lds16u(raw, delta + min(lane, C - 1) * T + 16 * blk);
-  }
+  const int o = L == TM ? delta + (16 * blk + (lane & 15)) * C + 16 * (lane >> 4) : delta + min(lane, C - 1) * T + 16 * blk;
+  if constexpr (AL) return *(const v4i*)(raw + o);
+  else return lds16u(raw, o);
 }
 
 // LDS-DMA of trial view v into the raw area: 1 KB pieces i = wave, wave + NW, ... (lane L's 16
@@ -274,13 +277,20 @@ __device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const V
   const int C = gp->C, T = gp->T, NB1 = gp->NB1;
   const int j = lane & 15, g = lane >> 4;
   constexpr int U = L == F32 ? 2 : 4;
+  // staged fragments all 16-byte aligned (wave-uniform: a scalar branch per group of U blocks)
+  const bool al = ST && v.delta == 0 && ((L == TM ? C : T) & 15) == 0;
   for (int b0 = wave; b0 < NB1; b0 += U * nw) {  // the blocks wave, wave + nw, ... (nw waves in layer 1)
     v4i raw[U];
+    if (al) {
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const int blk = min(b0 + u * nw, NB1 - 1);
-      if constexpr (ST) raw[u] = l1_fetch_lds<L>(sraw, v.delta, blk, C, T, lane);
-      else raw[u] = l1_fetch<L>(v, blk, C, T, lane, qs, qy);
+      for (int u = 0; u < U; u++) raw[u] = l1_fetch_lds<L, true>(sraw, v.delta, min(b0 + u * nw, NB1 - 1), C, T, lane);
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int blk = min(b0 + u * nw, NB1 - 1);
+        if constexpr (ST) raw[u] = l1_fetch_lds<L, false>(sraw, v.delta, blk, C, T, lane);
+        else raw[u] = l1_fetch<L>(v, blk, C, T, lane, qs, qy);
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
