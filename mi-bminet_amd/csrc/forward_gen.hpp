@@ -346,12 +346,12 @@ __device__ __forceinline__ int floor_el(int acc, float r, float c) {
   return __float_as_int(__builtin_amdgcn_fmed3f(g, FMAGIC_F, FMAGIC_F + (float)EMAX)) - FMAGIC_I;
 }
 
-template <bool XR, bool CB>
+template <bool RB, bool XR, bool CB>
 __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const int8_t* y1, int y1s, int8_t* y2, int y2s,
                                        const L2C& k, int wave, int lane) {
   constexpr int LO = CB ? -127 : -128;
   const int T8 = gp->T8, MT = gp->MT;
-  const bool rb = gp->rb != 0;
+  constexpr bool rb = RB;  // the blob's REORDER_BN flag (gp->rb), an instantiation
   const int n = lane & 31, h = lane >> 5;
   for (int mt = 0; mt < MT; mt++) {
     // both filters' B slices first: the six LDS reads overlap instead of each MFMA waiting on one
@@ -375,7 +375,7 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
 #pragma unroll
       for (int w = 0; w < 2; w++) {
         int sum = 0;
-        if (rb) {
+        if constexpr (rb) {
 #pragma unroll
           for (int i = 0; i < 8; i++) sum += max(acc[8 * w + i], k.thr[fi]);
           sum += k.off[fi];
@@ -416,7 +416,7 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
 #pragma unroll
       for (int s = 0; s < 2; s++) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(k.at[fi][s], bt[fi][s], acc, 0, 0, 0);
       int part = 0;
-      if (rb) {
+      if constexpr (rb) {
 #pragma unroll
         for (int i = 0; i < 4; i++) part += max(acc[i], k.thr[fi]);
       } else {
@@ -427,7 +427,7 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
       const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)part, (unsigned)part, false, false);
       const int tot = (int)(sw[0] + sw[1]);  // the whole window (rows g and g ^ 1 hold the same)
       int q;
-      if (rb) q = XR ? clampq(xdiv(tot + k.off[fi], k.m[fi], k.xs[fi]), LO) : clampq((int)((float)(tot + k.off[fi]) * k.r[fi]), LO);
+      if constexpr (rb) q = XR ? clampq(xdiv(tot + k.off[fi], k.m[fi], k.xs[fi]), LO) : clampq((int)((float)(tot + k.off[fi]) * k.r[fi]), LO);
       else q = tot >> 3;
       const int u = (p0 >> 3) + (g >> 1);
       if (!(g & 1) && u < T8) y2[(2 * wave + fi) * y2s + 8 + u] = (int8_t)q;
@@ -470,12 +470,12 @@ __device__ __forceinline__ void layer3(const GenParams* __restrict__ gp, const i
 
 // Layer 4 (layer4.c:51-149, FLIP_LAYERS): item (k, v): b = W4[k] . y3t[u] for u = 8 v .. 8 v + 7,
 // REORDER_BN: sum max(b, thr) + off, / fac; plain: sum max(tdiv(b + off >> 3, fac >> 3), 0) >> 3.
-template <bool XR, bool CB>
+template <bool RB, bool XR, bool CB>
 __device__ __forceinline__ void layer4(const GenParams* __restrict__ gp, const int8_t* y3, int8_t* y4,
                                        const SmallG* sg, int tid, int nthreads) {
   constexpr int LO = CB ? -127 : -128;
   const int T64 = gp->T64, T64A = gp->T64A;
-  const bool rb = gp->rb != 0;
+  constexpr bool rb = RB;  // the blob's REORDER_BN flag (gp->rb), an instantiation
   // output channel k = tid & 15 is the same for every item of this thread (nthreads % 16 == 0): its
   // constants are read once, all before the first item
   const int k = tid & 15;
@@ -496,7 +496,7 @@ __device__ __forceinline__ void layer4(const GenParams* __restrict__ gp, const i
       for (int q = 0; q < 4; q++) b[i] = __builtin_amdgcn_sdot4(a[q], w[q], b[i], false);
     }
     int sum = 0, y;
-    if (rb) {
+    if constexpr (rb) {
 #pragma unroll
       for (int i = 0; i < 8; i++) sum += max(b[i], thr);
       y = XR ? xdiv(sum + off, m, xs) : (int)((float)(sum + off) * r4);
@@ -580,8 +580,10 @@ __device__ __forceinline__ void setup(const GenParams* __restrict__ gp, int8_t* 
 
 // Fused forward over a batch of B trials (layout L), logits [B][N].
 // ST: int8 trials staged in LDS (the carve's raw area fits; the host picks the instantiation)
-template <int L, bool ST, bool XR, bool CB>
-__global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp, const int8_t* __restrict__ x,
+template <int L, bool ST, bool RB, bool XR, bool CB>
+// two workgroups per CU (4 waves per SIMD): at most 128 VGPRs
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_forward(
+    const GenParams* __restrict__ gp, const int8_t* __restrict__ x,
                                                  int8_t* __restrict__ out, int B, float qs, float qy) {
   static_assert(!ST || L != F32, "float32 trials are not staged");
   extern __shared__ v4i smem_v[];
@@ -627,7 +629,7 @@ __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp
       layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, wave, lane, qs, qy, NW - 1);
     } else if (bprev >= 0) {
       __builtin_amdgcn_s_setprio(wg::PRIO_L45);
-      layer4<XR, CB>(gp, y3, y4, sg, lane, 64);
+      layer4<RB, XR, CB>(gp, y3, y4, sg, lane, 64);
       wg::wave_sync_lds();
       layer5<CB>(gp, y4, smem + cv.w5, out + (size_t)bprev * N, 0, 1, lane);
     }
@@ -637,7 +639,7 @@ __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp
     const int bn = b + (int)gridDim.x;
     if (ST && bn < B) stage_trial(trial_view<L>(x, bn, C, T, xstride), sraw, cv.chunks, wave, lane);
     MIB_STAMP(1)
-    layer2<XR, CB>(gp, y1, cv.y1s, y2, cv.y2s, k2, wave, lane);
+    layer2<RB, XR, CB>(gp, y1, cv.y1s, y2, cv.y2s, k2, wave, lane);
     wg::wave_sync_lds();  // layer 3 of filter f reads only y2 row f, written by this wave
     MIB_STAMP(2)
     __builtin_amdgcn_s_setprio(wg::PRIO_L3);
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp
     bprev = b;
   }
   if (wave == NW - 1 && bprev >= 0) {  // the last trial's layers 4-5
-    layer4<XR, CB>(gp, y3, y4, sg, lane, 64);
+    layer4<RB, XR, CB>(gp, y3, y4, sg, lane, 64);
     wg::wave_sync_lds();
     layer5<CB>(gp, y4, smem + cv.w5, out + (size_t)bprev * N, 0, 1, lane);
   }
@@ -660,7 +662,7 @@ __global__ __launch_bounds__(NT) void k_forward(const GenParams* __restrict__ gp
 // Single-trial, single-layer kernel for the reference's per-layer entry points on the general
 // path: stage 1..5 = net_layerN, 6 = net_layer3_flip_inplace; reference layouts in and out (pads
 // zero).  Stage 1 takes the trial packed time-major [T][C] (the batched layout).
-template <bool XR, bool CB>
+template <bool RB, bool XR, bool CB>
 __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, const int8_t* __restrict__ in,
                                               int8_t* __restrict__ out, int stage) {
   extern __shared__ v4i smem_v[];
@@ -693,7 +695,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
       y1[f * cv.y1s + 32 + t] = in[f * TA + t];
     }
     __syncthreads();
-    layer2<XR, CB>(gp, y1, cv.y1s, y2, cv.y2s, k2, wave, lane);
+    layer2<RB, XR, CB>(gp, y1, cv.y1s, y2, cv.y2s, k2, wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T8A; i += NT) {
       const int f = i / T8A, u = i - f * T8A;
@@ -714,7 +716,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   } else if (stage == 4) {  // [T8][F2] -> [F2][T64_ALIGN]
     for (int i = tid; i < T8 * F2; i += NT) y3[i] = in[i];
     __syncthreads();
-    layer4<XR, CB>(gp, y3, y4, sg, tid, NT);
+    layer4<RB, XR, CB>(gp, y3, y4, sg, tid, NT);
     __syncthreads();
     for (int i = tid; i < F2 * T64A; i += NT) out[i] = y4[i];
   } else if (stage == 5) {  // [F2][T64_ALIGN] -> [N] (the pad columns read as zero)

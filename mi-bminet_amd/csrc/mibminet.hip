@@ -1159,47 +1159,57 @@ int launch_forward_t(DeviceState& ds, const DevParams* p, const int8_t* x, int8_
 }
 
 // General path: dynamic LDS from the run-time dimensions (gen::carve_of); the occupancy of each
-// (kernel, LDS size) is queried once.  Kernels may take more than the default 64 KB of dynamic LDS.
-template <class Kern>
-int gen_blocks_per_cu(Kern k, int lds) {
+// (kernel, LDS size) is queried once, and each kernel may take more than the default 64 KB of
+// dynamic LDS.  Keyed by the kernel's address: every instantiation has the same function type.
+int gen_blocks_per_cu(const void* k, int lds) {
   static std::mutex mu;
-  static std::vector<std::pair<int, int>> cache;  // (lds, blocks per CU)
-  static bool attr = false;
+  static std::vector<std::pair<const void*, int>> attr;          // kernels with the LDS attribute set
+  static std::vector<std::pair<std::pair<const void*, int>, int>> cache;  // ((kernel, lds), blocks per CU)
   std::lock_guard<std::mutex> lk(mu);
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
+  bool seen = false;
+  for (const auto& a : attr) seen = seen || a.first == k;
+  if (!seen) {
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr.emplace_back(k, 1);
   }
   for (const auto& c : cache)
-    if (c.first == lds) return c.second;
+    if (c.first.first == k && c.first.second == lds) return c.second;
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, gen::NT, (size_t)lds) != hipSuccess || n < 1) n = 1;
-  cache.emplace_back(lds, n);
+  cache.push_back({{k, lds}, n});
   return n;
 }
 
-template <int L, bool ST, bool XR, bool CB>
+template <int L, bool ST, bool RB, bool XR, bool CB>
 int launch_gen_q(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
                  hipStream_t st, int32_t* info, float qs) {
   const int lds = gen::carve_of(hg.C, hg.T, hg.N, hg.T8, hg.T64A, hg.NB1, hg.MT, hg.NTT, L).bytes;
-  const size_t cap = (size_t)ds.cus * (size_t)gen_blocks_per_cu(gen::k_forward<L, ST, XR, CB>, lds);
+  const void* kern = (const void*)gen::k_forward<L, ST, RB, XR, CB>;
+  const size_t cap = (size_t)ds.cus * (size_t)gen_blocks_per_cu(kern, lds);
   const int grid = (int)(B < cap ? B : cap);
   if (info) { info[0] = grid; info[1] = gen::NT; info[2] = lds; return NET_OK; }
   if (B == 0) return NET_OK;
   const float qy = qs > 0.0f ? 1.0f / qs : 0.0f;  // RN(1 / scale), as the specialised float kernels
-  hipLaunchKernelGGL((gen::k_forward<L, ST, XR, CB>), dim3(grid), dim3(gen::NT), (size_t)lds, st,
+  hipLaunchKernelGGL((gen::k_forward<L, ST, RB, XR, CB>), dim3(grid), dim3(gen::NT), (size_t)lds, st,
                      (const gen::GenParams*)p, x, y, (int)B, qs, qy);
   return hip_err(hipGetLastError());
 }
 
+// the blob's flags as instantiations: REORDER_BN, exact division, balanced clip
 template <int L, bool ST>
 int launch_gen_s(DeviceState& ds, const gen::GenParams& hg, const void* p, const int8_t* x, int8_t* y, size_t B,
                  hipStream_t st, int32_t* info, float qs) {
-  const bool cb = hg.lo == -127;
-  if (hg.xr) return cb ? launch_gen_q<L, ST, true, true>(ds, hg, p, x, y, B, st, info, qs)
-                       : launch_gen_q<L, ST, true, false>(ds, hg, p, x, y, B, st, info, qs);
-  return cb ? launch_gen_q<L, ST, false, true>(ds, hg, p, x, y, B, st, info, qs)
-            : launch_gen_q<L, ST, false, false>(ds, hg, p, x, y, B, st, info, qs);
+  const int sel = (hg.rb ? 4 : 0) | (hg.xr ? 2 : 0) | (hg.lo == -127 ? 1 : 0);
+  switch (sel) {
+    case 0: return launch_gen_q<L, ST, false, false, false>(ds, hg, p, x, y, B, st, info, qs);
+    case 1: return launch_gen_q<L, ST, false, false, true>(ds, hg, p, x, y, B, st, info, qs);
+    case 2: return launch_gen_q<L, ST, false, true, false>(ds, hg, p, x, y, B, st, info, qs);
+    case 3: return launch_gen_q<L, ST, false, true, true>(ds, hg, p, x, y, B, st, info, qs);
+    case 4: return launch_gen_q<L, ST, true, false, false>(ds, hg, p, x, y, B, st, info, qs);
+    case 5: return launch_gen_q<L, ST, true, false, true>(ds, hg, p, x, y, B, st, info, qs);
+    case 6: return launch_gen_q<L, ST, true, true, false>(ds, hg, p, x, y, B, st, info, qs);
+    default: return launch_gen_q<L, ST, true, true, true>(ds, hg, p, x, y, B, st, info, qs);
+  }
 }
 
 // int8 trials that fit in LDS run the staged instantiation (gen::carve_of)
@@ -1235,13 +1245,21 @@ int launch_layer(const Variant& v, const void* himg, const void* p, const int8_t
     const gen::GenParams& hg = *(const gen::GenParams*)himg;
     const int lds = gen::carve_of(hg.C, hg.T, hg.N, hg.T8, hg.T64A, hg.NB1, hg.MT, hg.NTT, 3).bytes;
     auto go = [&](auto kern) {
-      (void)gen_blocks_per_cu(kern, lds);  // the LDS attribute
+      (void)gen_blocks_per_cu((const void*)kern, lds);  // the LDS attribute
       hipLaunchKernelGGL(kern, dim3(1), dim3(gen::NT), (size_t)lds, st, (const gen::GenParams*)p, in, out, stage);
       return hip_err(hipGetLastError());
     };
-    const bool cb = hg.lo == -127;
-    if (hg.xr) return cb ? go(gen::k_layer<true, true>) : go(gen::k_layer<true, false>);
-    return cb ? go(gen::k_layer<false, true>) : go(gen::k_layer<false, false>);
+    const int sel = (hg.rb ? 4 : 0) | (hg.xr ? 2 : 0) | (hg.lo == -127 ? 1 : 0);
+    switch (sel) {
+      case 0: return go(gen::k_layer<false, false, false>);
+      case 1: return go(gen::k_layer<false, false, true>);
+      case 2: return go(gen::k_layer<false, true, false>);
+      case 3: return go(gen::k_layer<false, true, true>);
+      case 4: return go(gen::k_layer<true, false, false>);
+      case 5: return go(gen::k_layer<true, false, true>);
+      case 6: return go(gen::k_layer<true, true, false>);
+      default: return go(gen::k_layer<true, true, true>);
+    }
   }
   return dispatch(v, [&](auto k) {
     hipLaunchKernelGGL(wg::k_layer<decltype(k)>, dim3(1), dim3(wg::NTHREADS), 0, st, (const DevParams*)p, in, out, stage);
