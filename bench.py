@@ -63,10 +63,12 @@ def parse():
                     help="input layout: tc = time-major batched trials [B][stride] (net_model_compute_batch), "
                          "ct = channel-major [B][C][T] (net_model_compute_batch_ct, transposed inside the kernel), "
                          "f32 = float32 EEG [B][C][T] (net_model_compute_batch_f32, quantised inside the kernel)")
-    ap.add_argument("--params", default="synthetic", choices=("synthetic", "extreme"),
+    ap.add_argument("--params", default="synthetic", choices=("synthetic", "extreme", "rails"),
                     help="synthetic: calibrated seeded weights (the benchmark set, float requant kernels); "
                          "extreme: requant factors and offsets far outside the float envelope "
-                         "(ParamSet.synthetic_extreme, the exact integer-division kernels)")
+                         "(ParamSet.synthetic_extreme, the exact integer-division kernels); "
+                         "rails: the same with only constant (rail / zero / suppressed) filters out of "
+                         "the envelope, which the loader folds (float kernels)")
     ap.add_argument("--force-general", action="store_true",
                     help="run the run-time-dimension kernels even on a compiled geometry (comparison)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -230,8 +232,8 @@ def main():
 
     kw = dict(C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"], reorder_bn=a.variant != "plain_bn",
               clip_balanced=a.variant == "clip_balanced")
-    if a.params == "extreme":
-        ps = ParamSet.synthetic_extreme(a.seed, **kw)
+    if a.params in ("extreme", "rails"):
+        ps = ParamSet.synthetic_extreme(a.seed, mids=6 if a.params == "extreme" else 0, **kw)
     else:
         ps = ParamSet.synthetic(a.seed, N=cfg.get("N", 4), **kw)
     if a.force_general and not STUB:
@@ -349,7 +351,7 @@ def main():
             # (time-major under the config's key, other input layouts under "<config>_<layout>")
             key = a.config if a.layout == "tc" else f"{a.config}_{a.layout}"
             tc = tj.get("configs", {}).get(key, tj if tj.get("config") == key else {})
-            if tc.get("batch") == B and a.variant == "canonical" and a.params == "synthetic":
+            if tc.get("batch") == B and a.variant == "canonical" and a.params == "synthetic" and not a.force_general:
                 traffic = tc["hbm_bytes_per_launch"]
         except (OSError, ValueError, KeyError):
             pass

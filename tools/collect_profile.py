@@ -43,7 +43,11 @@ def main():
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(one(f"{src}/trace/**/*kernel_stats.csv"), f"{prof}/{tag}_kernel_stats.csv")
-    for cfg in ("b22", "c64", "d22", "p64", "b22_ct", "c64_ct", "b22_f32"):
+    g = glob.glob(f"{src}/trace_g19/**/*kernel_stats.csv", recursive=True)
+    if g:  # the general kernels (config g19)
+        shutil.copy(g[0], f"{prof}/{tag}_kernel_stats_g19.csv")
+    for cfg in ("b22", "c64", "d22", "p64", "b22_ct", "c64_ct", "b22_f32", "g19", "g38", "p64l", "b22_extreme",
+                "b22_rails"):
         p = f"{src}/bench_{cfg}.json"
         if os.path.exists(p):
             lines = [l for l in open(p) if l.startswith("{")]
@@ -54,12 +58,15 @@ def main():
     # skip the first (warm-up) dispatch
     med = lambda v: sorted(v[1:] or v)[len(v[1:] or v) // 2]  # noqa: E731
     alg = {"b22": 22 * 1125 + 4, "c64": 64 * 1000 + 4, "d22": 22 * 1125 + 4,
-           "b22_ct": 22 * 1125 + 4, "c64_ct": 64 * 1000 + 4, "b22_f32": 4 * 22 * 1125 + 4}
-    kern = {"b22": "22,1125,RB=1,CB=0", "c64": "64,1000,RB=1,CB=0", "d22": "22,1125,RB=1,CB=0",
-            "b22_ct": "22,1125,RB=1,CB=0,CT=1", "c64_ct": "64,1000,RB=1,CB=0,CT=1",
-            "b22_f32": "22,1125,RB=1,CB=0,CT=1,FQ=1"}
+           "b22_ct": 22 * 1125 + 4, "c64_ct": 64 * 1000 + 4, "b22_f32": 4 * 22 * 1125 + 4,
+           "g19": 19 * 1125 + 3, "g38": 38 * 480 + 2, "p64l": 64 * 960 + 4}
+    kern = {"b22": "k_forward<Cfg<22,1125,RB=1,CB=0>>", "c64": "k_forward<Cfg<64,1000,RB=1,CB=0>>",
+            "d22": "k_forward<Cfg<22,1125,RB=1,CB=0>>", "b22_ct": "k_forward<Cfg<22,1125,RB=1,CB=0,CT=1>>",
+            "c64_ct": "k_forward<Cfg<64,1000,RB=1,CB=0,CT=1>>", "b22_f32": "k_forward<Cfg<22,1125,RB=1,CB=0,CT=1,FQ=1>>",
+            "g19": "gen::k_forward<TM,ST,RB,float,CB=0> (19x1125, N=3)", "g38": "gen::k_forward<TM,ST,RB,float,CB=0> (38x480, N=2)",
+            "p64l": "gen::k_forward<TM,ST,RB,float,CB=0> (64x960, N=4)"}
     configs = {}
-    for cfg in ("b22", "c64", "d22", "b22_ct", "c64_ct", "b22_f32"):
+    for cfg in ("b22", "c64", "d22", "b22_ct", "c64_ct", "b22_f32", "g19", "g38", "p64l"):
         wf = glob.glob(f"{src}/pmc_write_{cfg}/**/*counter_collection.csv", recursive=True)
         rq = glob.glob(f"{src}/pmc_rdreq_{cfg}/**/*counter_collection.csv", recursive=True)
         if not (wf and rq):
@@ -77,7 +84,7 @@ def main():
         # sizes, if any, are reported as the remainder and not counted); writes WRITE_SIZE (kB)
         read_bytes = 32 * n[rcols[1]] + 64 * n[rcols[2]] + 128 * n[rcols[3]]
         write_bytes = med(write) * 1024
-        tc = {"batch": 65536, "kernel": "k_forward<Cfg<%s>>" % kern[cfg],
+        tc = {"batch": 65536, "kernel": kern[cfg],
               "rdreq": n, "rdreq_other": n[rcols[0]] - n[rcols[1]] - n[rcols[2]] - n[rcols[3]],
               "read_bytes": read_bytes, "write_bytes": write_bytes,
               "alg_bytes_per_launch": alg[cfg] * 65536,
