@@ -17,7 +17,9 @@ own steps (host clock around them, HIP events on its launch stream), then the ra
 average kernel duration from HIP events on the launch stream.  ``cpu_baseline`` times the C
 restatement of the reference forward (oracle/, kind "port") on the host cores (rank 0, N = 1),
 and its logits on that sample are compared with the timed batch's: ``parity`` = trials checked and
-mismatches; any mismatch makes the run exit non-zero (after printing the line).
+mismatches; any mismatch makes the run exit non-zero (after printing the line).  Without a timed
+baseline (--no-cpu-baseline, or N > 1) the oracle still checks the whole batch (rank 0's shard),
+untimed, after the timed steps.
 """
 import argparse
 import json
@@ -179,6 +181,21 @@ def cpu_baseline(ps, x_dev, seconds):
             "affinity_mask_threads": mask,
             "host_cpus": {"affinity": ncpu, "os_cpu_count": os.cpu_count(), "cgroup_cpu_quota": quota,
                           "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}}
+
+
+def oracle_logits(ps, x_dev, n):
+    """The checker of the CPU leg when the baseline is not timed (--no-cpu-baseline, or N > 1: rank
+    0's own shard): the oracle's logits of the first n trials, one thread per usable CPU."""
+    sys.path.insert(0, ROOT)
+    import oracle  # test infrastructure: the checker, never the thing measured
+
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    quota = _cpu_quota()
+    threads = ncpu if quota is None else max(1, min(ncpu, int(quota + 0.999)))
+    return oracle.COracle(ps).batch(x_dev[:n].cpu().numpy(), nthreads=threads)
 
 
 def logit_parity(y_host, want):
@@ -412,6 +429,11 @@ def main():
         if world == 1 and not a.no_cpu_baseline and not STUB:
             want, out["cpu_baseline"] = cpu_baseline(ps, x, a.cpu_seconds)
             out["parity"] = logit_parity(y[: want.shape[0]].cpu().numpy(), want)
+        elif not STUB:  # no timed baseline: the whole batch (rank 0's shard) is still checked
+            want = oracle_logits(ps, x, B)
+            out["parity"] = logit_parity(y.cpu().numpy(), want)
+            if world > 1:
+                out["parity"]["against"] += " (rank 0's shard)"
         print(json.dumps(out), flush=True)
         if out["parity"] and out["parity"]["mismatches"]:
             failed = "bench.py: the timed batch's logits differ from the oracle's on %d of %d trials" % (

@@ -113,7 +113,11 @@ int net_params_load(const void* blob, size_t len);
  * proven float form (NET_PATH_EXACT), else 0; info[2] = its filter, else -1; info[3] = the
  * compiled geometry (0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480), -1 on the general path; info[4] = 1
  * when the set divides exactly at layers 1-4 (NET_PATH_EXACT, or NET_PATH_GENERAL without a proven
- * float form for every requant), 0 when it runs the proven float requant.  info holds 5 entries. */
+ * float form for every requant), 0 when it runs the proven float requant.  info holds 5 entries.
+ * A layer-1, -2 or -4 filter whose output is one constant over its whole reachable range (an
+ * offset past the weights' reach, a factor that sends every sum to zero, a suppressed ReLU) is
+ * folded into an equivalent constant filter before the choice, so such filters alone never force
+ * exact division; info[1] / info[2] name a filter whose output varies. */
 #define NET_PATH_FLOAT 0
 #define NET_PATH_EXACT 1
 #define NET_PATH_GENERAL 2
