@@ -182,3 +182,48 @@ def test_folded_rail_sets_on_the_float_kernels(C, T, rb, cb, gpu):
     y4 = co.layer4(y3t)
     np.testing.assert_array_equal(lib.net_layer4(y3t), y4)
     np.testing.assert_array_equal(lib.net_model_compute(xa), co.model(xa))
+
+
+def test_xr_divisor_extremes_on_varying_filters(gpu):
+    """The exact-division kernels' divisor magics at their ends: layer-1 filters with
+    factors 1, -1, 2^31 - 1 and -(2^31 - 1) whose outputs vary (so none is folded), in a set that
+    runs exact division, against the oracle.  Crafted trials reach each filter's range end
+    (dot = its maximum or minimum), where trunc(v / +-(2^31 - 1)) = +-1."""
+    import torch
+
+    I32_MAX, I32_MIN = 2 ** 31 - 1, -(2 ** 31)
+    ps = ParamSet.synthetic_extreme(314, C=22, T=1125, mids=6)
+    from mibminet.params import dot_ranges
+    r1 = dot_ranges(ps)[0]
+    w1 = ps.w1().astype(np.int64)  # [F][C]
+    picks = {}
+    for f, (fac, off_of) in zip((1, 4, 7, 10), (
+            (1, lambda lo, hi: -((lo + hi) // 2)),
+            (-1, lambda lo, hi: -((lo + hi) // 2)),
+            (I32_MAX, lambda lo, hi: I32_MAX - hi),
+            (-I32_MAX, lambda lo, hi: I32_MIN + 1 - lo))):
+        lo, hi = r1[f]
+        ps.l1_factor[f] = np.int32(fac)
+        ps.l1_offset[f] = np.int32(off_of(lo, hi))
+        picks[f] = fac
+    ps.__post_init__()
+    lib.params_load(ps)
+    assert lib.params_exact_division()
+    rng = np.random.default_rng(5)
+    B = 40
+    x = rng.integers(-128, 128, size=(B, 22, 1125)).astype(np.int8)
+    for i, f in enumerate((7, 10)):  # every sample at the filter's dot maximum (7) / minimum (10)
+        top = np.where(w1[f] > 0, 127, -128) if f == 7 else np.where(w1[f] > 0, -128, 127)
+        x[i] = top[:, None].astype(np.int8)
+    xp = pack_trials(x)
+    co = oracle.COracle(ps)
+    assert np.array_equal(lib.forward_torch(torch.from_numpy(xp).cuda()).cpu().numpy(), co.batch(xp, nthreads=NT))
+    d = ps.dims
+    for i in (0, 1, 2):
+        xa = oracle.to_tc_align(x[i], d.C_ALIGN)
+        y1 = lib.net_layer1(xa)
+        np.testing.assert_array_equal(y1, co.layer1(xa))
+        if i == 0:
+            assert (y1[7, : d.T] == 1).all()   # trunc(INT32_MAX / INT32_MAX)
+        if i == 1:
+            assert (y1[10, : d.T] == 1).all()  # trunc((INT32_MIN + 1) / -INT32_MAX)
