@@ -250,7 +250,7 @@ def main():
     kw = dict(C=cfg["C"], T=cfg["T"], weight_bits=cfg["wbits"], reorder_bn=a.variant != "plain_bn",
               clip_balanced=a.variant == "clip_balanced")
     if a.params in ("extreme", "rails"):
-        ps = ParamSet.synthetic_extreme(a.seed, mids=6 if a.params == "extreme" else 0, **kw)
+        ps = ParamSet.synthetic_extreme(a.seed, mids=6 if a.params == "extreme" else 0, N=cfg.get("N", 4), **kw)
     else:
         ps = ParamSet.synthetic(a.seed, N=cfg.get("N", 4), **kw)
     if a.force_general and not STUB:
@@ -262,7 +262,7 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(a.seed * 1000 + rank)
     sync = (lambda: None) if STUB else (lambda: torch.cuda.synchronize(dev))
-    C, T, N = cfg["C"], cfg["T"], cfg.get("N", 4)
+    C, T, N = cfg["C"], cfg["T"], ps.dims.N  # the logits' row length is the loaded set's
     if STUB:  # host int8 trials whatever the layout (no device, no library compute)
         x = torch.randint(-128, 128, (B, stride), dtype=torch.int8, generator=g)
     elif a.layout == "f32":

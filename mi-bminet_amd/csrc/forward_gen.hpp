@@ -50,9 +50,8 @@ enum Layout { TM = 0, CT = 1, F32 = 2 };
 
 // Per-filter constants read by layers 3 and 4 of every wave: copied into LDS once per workgroup.
 struct SmallG {
-  int l3_w[F2][4][8];     // layer 3: output phase k = u & 3: byte q < 20 of the 20-byte window at
-                          // u & ~3 meets tap W3t[q - k - 1] (dwords 0..4; 5..7 zero)
-  int l4_w[F2][4];        // layer 4: weight row k, 16 bytes
+  v4i l3_a[NW][64];       // layer 3: wave w's A fragment per lane (filters 2w, 2w + 1; layer3)
+  v4i l4_b[64];           // layer 4: the block-diagonal B fragment per lane (layer4)
   int l4_thr[F2];         // REORDER_BN: -(offset >> 3); plain: unused
   int l4_off[F2];         // REORDER_BN: offset; plain: offset >> 3
   unsigned l4_m[F2];      // XR: xdiv magic of factor (plain: factor >> 3)
@@ -60,7 +59,7 @@ struct SmallG {
   float l4_r[F2];         // float form: reciprocal (REORDER_BN) / floor-form r (plain)
   float l4_c[F2];         // plain floor form: c
   int l4_ci[F2];          // plain floor form: magic bits + offset >> 3
-  int pad[4];
+  int zero16[4];          // 16 zero bytes (layer 3's off-diagonal K halves)
 };
 static_assert(sizeof(SmallG) % 16 == 0, "SmallG is copied in 16-byte pieces");
 
@@ -68,7 +67,9 @@ static_assert(sizeof(SmallG) % 16 == 0, "SmallG is copied in 16-byte pieces");
 struct GenParams {
   int C, T, N, T8;
   int T64, T64A, NB1, MT;       // NB1: layer-1 blocks of 16 samples; MT: full layer-2 tiles of 1024 outputs
-  int NTT, pad2[3];             // layer-2 tail tiles of 256 outputs per filter past the MT full tiles
+  int NTT;                      // layer-2 tail tiles of 256 outputs per filter past the MT full tiles
+  int K7;                       // layer-1 blocks of the last wave (its layers 4-5 first), the trial's last ones
+  int pad2[2];
   int rb, lo, xstride, xr;      // REORDER_BN branches; lower clip bound; time-major trial stride;
                                 // exact division (no proven float form for some requant)
   unsigned l3_m;
@@ -253,7 +254,7 @@ __device__ __forceinline__ void stage_trial(const View& v, int8_t* raw, int chun
   for (int i = wave; i < chunks; i += NW) wg::dma_b128(v.r, 1024 * i + 16 * lane, 0, base + 1024 * i);
 }
 
-// Layer 1: this wave's blocks blk = wave, wave + NW, ... -> y1 rows (position 32 + t).  Loads of
+// Layer 1: the blocks first, first + nw, ... < end -> y1 rows (position 32 + t).  Loads of
 // U blocks are issued before their MFMAs.
 // Requant of one layer-1 output (acc = dot + offset, or its float-magic form): exact division
 // (XR) or fma(acc bits, r, c) = RN((dot + off) r), truncated (the host proves it equals C's
@@ -284,23 +285,23 @@ struct L1C {  // a lane's layer-1 constants (filter lane & 15)
 // (slots past NB1 re-read the last block; their results are not stored).
 template <int L, bool ST, bool XR, bool CB>
 __device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const View& v, const int8_t* sraw, int8_t* y1,
-                                       int y1s, int8_t* stg, const L1C& k, int wave, int lane, float qs, float qy,
-                                       int nw) {
+                                       int y1s, int8_t* stg, const L1C& k, int first, int nw, int end, int lane,
+                                       float qs, float qy) {
   const int C = gp->C, T = gp->T, NB1 = gp->NB1;
   const int j = lane & 15, g = lane >> 4;
   constexpr int U = L == F32 ? 2 : 4;
   // staged fragments all 16-byte aligned (wave-uniform: a scalar branch per group of U blocks)
   const bool al = ST && v.delta == 0 && ((L == TM ? C : T) & 15) == 0;
   const L1Src src = l1_src<L>(sraw, v.delta, C, T, lane);
-  for (int b0 = wave; b0 < NB1; b0 += U * nw) {  // the blocks wave, wave + nw, ... (nw waves in layer 1)
+  for (int b0 = first; b0 < end; b0 += U * nw) {  // the blocks first, first + nw, ... < end
     v4i raw[U];
     if (al) {
 #pragma unroll
-      for (int u = 0; u < U; u++) raw[u] = l1_fetch_lds<true>(src, min(b0 + u * nw, NB1 - 1));
+      for (int u = 0; u < U; u++) raw[u] = l1_fetch_lds<true>(src, min(b0 + u * nw, end - 1));
     } else {
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int blk = min(b0 + u * nw, NB1 - 1);
+        const int blk = min(b0 + u * nw, end - 1);
         if constexpr (ST) raw[u] = l1_fetch_lds<false>(src, blk);
         else raw[u] = l1_fetch<L>(v, blk, C, T, lane, qs, qy);
       }
@@ -308,7 +309,7 @@ __device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const V
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const int blk = b0 + u * nw;
-      if (blk < NB1) {  // wave-uniform
+      if (blk < end) {  // wave-uniform
         const v4i a = L == TM ? raw[u] : wg::stage_block<TrK>(raw[u], stg, lane);
         const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, k.wf, (v4i){k.off, k.off, k.off, k.off}, 0, 0, 0);
         // lane column j = filter j, rows 4 g + r = samples 16 blk + 4 g + r
@@ -436,78 +437,94 @@ __device__ __forceinline__ void layer2(const GenParams* __restrict__ gp, const i
 }
 
 // Layer 3 (layer3.c:49-79, conv.c:105): output u of filter f = sum_j y2p[u + j] W3t[j], y2p[i] at
-// row byte i + 1; four outputs u0 .. u0 + 3 per item from row bytes u0 .. u0 + 19.  Written to
-// y3t[u][f] (net_layer3_flip_inplace as index math).
+// row byte i + 1, so a block of 16 outputs from u0 reads row bytes u0 + 1 .. u0 + 31.  One MFMA
+// i32_16x16x64_i8 per 128 outputs of the wave's two filters, with a block-diagonal K as in the
+// compiled kernels (forward_wg.hpp, layer3): columns 0..7 are filter 2w's blocks j = 0..7,
+// columns 8..15 filter 2w+1's; K-slots 0..31 carry filter 2w's 32-byte windows and band
+// (A[r][k] = W3t[k - r - 1], SmallG::l3_a), slots 32..63 filter 2w+1's; a lane whose K half
+// belongs to the other filter reads 16 zero bytes.  D lane (col, g) holds outputs
+// u0 + 4 g .. u0 + 4 g + 3 of its column's block, written to y3t[u][f] (net_layer3_flip_inplace as
+// index math); windows past T8 read zero pads or other rows, and their outputs are not stored.
 template <bool XR, bool CB>
-__device__ __forceinline__ void layer3(const GenParams* __restrict__ gp, const int8_t* y2, int y2s, int8_t* y3,
-                                       int wave, int lane) {
+__device__ __forceinline__ void layer3(const GenParams* __restrict__ gp, const SmallG* sg, const int8_t* y2, int y2s,
+                                       int8_t* y3, int wave, int lane) {
   constexpr int LO = CB ? -127 : -128;
   const int T8 = gp->T8;
   const unsigned m = gp->l3_m;
   const int xs = gp->l3_xs;
   const float r = gp->l3_r, c = gp->l3_c;
+  const int col = lane & 15, g = lane >> 4, fi = col >> 3, j = col & 7;
+  const int f = 2 * wave + fi;
+  asm volatile("" ::: "memory");  // the A fragment is read here, not kept in registers across the trial loop
+  const v4i a = sg->l3_a[wave][lane];
+  // this lane's 16 window bytes: its column's filter row when the K half is that filter's, else zeros
+  const int8_t* src = (g >> 1) == fi ? y2 + f * y2s + 16 * j + 16 * (g & 1) : (const int8_t*)sg->zero16;
+  const int step = (g >> 1) == fi ? 128 : 0;
+  const int ci = XR ? 0 : FMAGIC_I;  // float form: |conv| < 2^22 rides on the magic (exact)
+  for (int t = 0; 128 * t < T8; t++) {
+    const v4i b = *(const v4i*)(src + step * t);
+    const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, (v4i){ci, ci, ci, ci}, 0, 0, 0);
+    const int u0 = 128 * t + 16 * j + 4 * g;
 #pragma unroll
-  for (int fi = 0; fi < 2; fi++) {
-    const int f = 2 * wave + fi;  // wave-uniform: the taps come by scalar loads
-    const int* w = &gp->sg.l3_w[f][0][0];
-    for (int u0 = 4 * lane; u0 < T8; u0 += 256) {
-      const int* row = (const int*)(y2 + f * y2s + u0);
-      int d[5];
-#pragma unroll
-      for (int i = 0; i < 5; i++) d[i] = row[i];
-      // no branch inside: outputs past T8 land in rows T8 .. T8 + 2, which nothing reads
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        int acc = XR ? 0 : FMAGIC_I;  // float form: |conv| < 2^22 rides on the magic (exact)
-#pragma unroll
-        for (int i = 0; i < 5; i++) acc = __builtin_amdgcn_sdot4(d[i], w[8 * k + i], acc, false);
-        const int y = XR ? xdiv(acc, m, xs) : (int)__builtin_fmaf(__int_as_float(acc), r, c);
-        y3[16 * (u0 + k) + f] = (int8_t)clampq(y, LO);
-      }
+    for (int q = 0; q < 4; q++) {
+      const int y = XR ? xdiv(acc[q], m, xs) : (int)__builtin_fmaf(__int_as_float(acc[q]), r, c);
+      if (u0 + q < T8) y3[16 * (u0 + q) + f] = (int8_t)clampq(y, LO);
     }
   }
 }
 
-// Layer 4 (layer4.c:51-149, FLIP_LAYERS): item (k, v): b = W4[k] . y3t[u] for u = 8 v .. 8 v + 7,
+// Layer 4 (layer4.c:51-149, FLIP_LAYERS): b[k][u] = W4[k] . y3t[u], pooled over u = 8 v .. 8 v + 7;
 // REORDER_BN: sum max(b, thr) + off, / fac; plain: sum max(tdiv(b + off >> 3, fac >> 3), 0) >> 3.
+// One MFMA i32_32x32x32_i8 per part p of 64 samples, as the compiled kernels' layer 4: A row i of
+// lane (i, h) = y3t[64 p + 32 h + n(i)] in K-slots 16 h .. 16 h + 15 (n(i) = 16 ((i >> 2) & 1) +
+// 4 (i >> 3) + (i & 3)); B block-diagonal (SmallG::l4_b: column c < 16 = channel c on slots 0..15,
+// column c >= 16 = channel c - 16 on slots 16..31).  Lane (c, h) register r then holds
+// b[c & 15][64 p + 32 (c >> 4) + 16 h + r]: the two pool windows v = 8 p + 4 (c >> 4) + 2 h + {0, 1}.
+// Parts p0, p0 + pstep, ...; samples past T8 read other LDS bytes and feed only windows v >= T64,
+// which are not stored.
 template <bool RB, bool XR, bool CB>
 __device__ __forceinline__ void layer4(const GenParams* __restrict__ gp, const int8_t* y3, int8_t* y4,
-                                       const SmallG* sg, int tid, int nthreads) {
+                                       const SmallG* sg, int lane, int p0, int pstep) {
   constexpr int LO = CB ? -127 : -128;
   const int T64 = gp->T64, T64A = gp->T64A;
   constexpr bool rb = RB;  // the blob's REORDER_BN flag (gp->rb), an instantiation
-  // output channel k = tid & 15 is the same for every item of this thread (nthreads % 16 == 0): its
-  // constants are read once, all before the first item
-  const int k = tid & 15;
-  const v4i w = *(const v4i*)sg->l4_w[k];
+  // the lane's addresses and constants are derived and read here, per call: hoisted out of the
+  // trial loop they were held in registers (and spilled in the plain float builds)
+  int ln;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(ln) : "v"(lane));
+  const int c = ln & 31, h = ln >> 5, k = c & 15;
+  const int i = c;  // A row of this lane
+  const int n = 16 * ((i >> 2) & 1) + 4 * (i >> 3) + (i & 3);
+  asm volatile("" ::: "memory");
+  const v4i bw = sg->l4_b[ln];
   const int thr = sg->l4_thr[k], off = sg->l4_off[k], xs = sg->l4_xs[k];
   const unsigned m = sg->l4_m[k];
   const float r4 = sg->l4_r[k], c4 = sg->l4_c[k];
-  const int ci4 = sg->l4_ci[k];
-  for (int it = tid; it < F2 * T64; it += nthreads) {  // items tid, tid + nthreads, ...
-    const int v = it >> 4;
-    // the eight rows' reads and dot products first (no branch between them), then the branch
-    int b[8];
+  const int ci = (!rb && !XR) ? sg->l4_ci[k] : 0;  // plain float form: the floor form's C-init
+  const int NP = (T64 + 7) / 8;
+  for (int p = p0; p < NP; p += pstep) {
+    const v4i a = *(const v4i*)(y3 + 16 * (64 * p + 32 * h + n));
+    const v16i acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bw, (v16i){ci, ci, ci, ci, ci, ci, ci, ci, ci, ci, ci, ci, ci, ci, ci, ci}, 0, 0, 0);
+    int q[2];
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const v4i a = *(const v4i*)(y3 + 16 * (8 * v + i));
-      b[i] = 0;
+    for (int w = 0; w < 2; w++) {
+      int sum = 0;
+      if constexpr (rb) {
 #pragma unroll
-      for (int q = 0; q < 4; q++) b[i] = __builtin_amdgcn_sdot4(a[q], w[q], b[i], false);
+        for (int e = 0; e < 8; e++) sum += max(acc[8 * w + e], thr);
+        q[w] = clampq(XR ? xdiv(sum + off, m, xs) : (int)((float)(sum + off) * r4), LO);
+      } else {
+        // plain: layer4.c:113-118 clips no element (the float form clamps at 1024, past which the
+        // result saturates anyway)
+#pragma unroll
+        for (int e = 0; e < 8; e++) sum += XR ? max(xdiv(acc[8 * w + e] + off, m, xs), 0) : floor_el<1024>(acc[8 * w + e], r4, c4);
+        q[w] = clampq(sum >> 3, LO);
+      }
     }
-    int sum = 0, y;
-    if constexpr (rb) {
-#pragma unroll
-      for (int i = 0; i < 8; i++) sum += max(b[i], thr);
-      y = XR ? xdiv(sum + off, m, xs) : (int)((float)(sum + off) * r4);
-    } else {
-      // plain: layer4.c:113-118 clips no element (the float form clamps at 1024, past which the
-      // result saturates anyway)
-#pragma unroll
-      for (int i = 0; i < 8; i++) sum += XR ? max(xdiv(b[i] + off, m, xs), 0) : floor_el<1024>(b[i] + ci4, r4, c4);
-      y = sum >> 3;
-    }
-    y4[k * T64A + v] = (int8_t)clampq(y, LO);
+    const int v = 8 * p + 4 * (c >> 4) + 2 * h;
+    int8_t* dst = y4 + k * T64A + v;
+    if (v + 1 < T64) *(unsigned short*)dst = (unsigned short)((q[0] & 255) | ((q[1] & 255) << 8));
+    else if (v < T64) *dst = (int8_t)q[0];
   }
 }
 
@@ -600,7 +617,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   int8_t* y3 = smem + cv.y3;
   int8_t* y4 = smem + cv.y4;
   int8_t* stg = smem + cv.stg + 1024 * wave;
-  const int C = gp->C, T = gp->T, N = gp->N, xstride = gp->xstride;
+  const int C = gp->C, T = gp->T, N = gp->N, xstride = gp->xstride, NB1 = gp->NB1, K7 = gp->K7;
   // int8 trials staged in LDS (cv.raw >= 0, uniform): the first one now; after that each trial a
   // grid stride ahead, by LDS-DMA issued after barrier A (layer 1 has read the area) and waited for
   // before barrier B, so it lands during layers 2-3 and no wave waits on HBM in layer 1
@@ -626,12 +643,19 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // dependency chain of the interval and issue first; layer 1 ahead of the other workgroup's 2-3
     if (wave < NW - 1) {
       __builtin_amdgcn_s_setprio(wg::PRIO_L1);
-      layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, wave, lane, qs, qy, NW - 1);
-    } else if (bprev >= 0) {
-      __builtin_amdgcn_s_setprio(wg::PRIO_L45);
-      layer4<RB, XR, CB>(gp, y3, y4, sg, lane, 64);
-      wg::wave_sync_lds();
-      layer5<CB>(gp, y4, smem + cv.w5, out + (size_t)bprev * N, 0, 1, lane);
+      layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, wave, NW - 1, NB1 - K7, lane, qs, qy);
+    } else {
+      if (bprev >= 0) {
+        __builtin_amdgcn_s_setprio(wg::PRIO_L45);
+        layer4<RB, XR, CB>(gp, y3, y4, sg, lane, 0, 1);
+        wg::wave_sync_lds();
+        layer5<CB>(gp, y4, smem + cv.w5, out + (size_t)bprev * N, 0, 1, lane);
+      }
+      // then the trial's last K7 layer-1 blocks (host-balanced against layers 4-5)
+      if (K7 > 0) {
+        __builtin_amdgcn_s_setprio(wg::PRIO_L1);
+        layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, NB1 - K7, 1, NB1, lane, qs, qy);
+      }
     }
     __builtin_amdgcn_s_setprio(0);
     MIB_STAMP(0)
@@ -643,7 +667,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     wg::wave_sync_lds();  // layer 3 of filter f reads only y2 row f, written by this wave
     MIB_STAMP(2)
     __builtin_amdgcn_s_setprio(wg::PRIO_L3);
-    layer3<XR, CB>(gp, y2, cv.y2s, y3, wave, lane);
+    layer3<XR, CB>(gp, sg, y2, cv.y2s, y3, wave, lane);
     __builtin_amdgcn_s_setprio(0);
     MIB_STAMP(3)
     if (ST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of the next trial
@@ -652,7 +676,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     bprev = b;
   }
   if (wave == NW - 1 && bprev >= 0) {  // the last trial's layers 4-5
-    layer4<RB, XR, CB>(gp, y3, y4, sg, lane, 64);
+    layer4<RB, XR, CB>(gp, y3, y4, sg, lane, 0, 1);
     wg::wave_sync_lds();
     layer5<CB>(gp, y4, smem + cv.w5, out + (size_t)bprev * N, 0, 1, lane);
   }
@@ -683,7 +707,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   __syncthreads();
   if (stage == 1) {  // [T][C] packed -> [F1][T_ALIGN]
     const View v = trial_view<TM>(in, 0, C, T, gp->xstride);
-    layer1<TM, false, XR, CB>(gp, v, nullptr, y1, cv.y1s, nullptr, k1, wave, lane, 0.0f, 0.0f, NW);
+    layer1<TM, false, XR, CB>(gp, v, nullptr, y1, cv.y1s, nullptr, k1, wave, NW, gp->NB1, lane, 0.0f, 0.0f);
     __syncthreads();
     for (int i = tid; i < F2 * TA; i += NT) {
       const int f = i / TA, t = i - f * TA;
@@ -707,7 +731,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
       y2[f * cv.y2s + 8 + u] = in[f * T8A + u];
     }
     __syncthreads();
-    layer3<XR, CB>(gp, y2, cv.y2s, y3, wave, lane);
+    layer3<XR, CB>(gp, sg, y2, cv.y2s, y3, wave, lane);
     __syncthreads();
     for (int i = tid; i < F2 * T8A; i += NT) {
       const int f = i / T8A, u = i - f * T8A;
@@ -716,7 +740,7 @@ __global__ __launch_bounds__(NT) void k_layer(const GenParams* __restrict__ gp, 
   } else if (stage == 4) {  // [T8][F2] -> [F2][T64_ALIGN]
     for (int i = tid; i < T8 * F2; i += NT) y3[i] = in[i];
     __syncthreads();
-    layer4<RB, XR, CB>(gp, y3, y4, sg, tid, NT);
+    layer4<RB, XR, CB>(gp, y3, y4, sg, lane, wave, NW);
     __syncthreads();
     for (int i = tid; i < F2 * T64A; i += NT) out[i] = y4[i];
   } else if (stage == 5) {  // [F2][T64_ALIGN] -> [N] (the pad columns read as zero)

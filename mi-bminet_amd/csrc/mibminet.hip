@@ -746,6 +746,11 @@ int build_genparams(HostParams& hp, gen::GenParams& gp) {
   const int rest = NB2 % 32;
   gp.MT = NB2 / 32 + (rest > 16 ? 1 : 0);
   gp.NTT = (rest > 0 && rest <= 16) ? (2 * rest + 15) / 16 : 0;
+  // the last wave runs layers 4-5 (about two layer-1 blocks' time per 64 samples of layer 4, on
+  // the phase stamps) and then the trial's last K7 layer-1 blocks; the other seven share the rest:
+  // (NB1 - K7) / 7 = 2 NP + K7, NP = layer-4 parts
+  const int NP = (T64 + 7) / 8;
+  gp.K7 = std::max(0, (gp.NB1 - 14 * NP) / 8);
   gp.rb = hp.reorder_bn ? 1 : 0;
   gp.lo = hp.clip_balanced ? -127 : -128;
   gp.xstride = (int)(((size_t)C * d.T + 15) / 16 * 16);
@@ -777,18 +782,28 @@ int build_genparams(HostParams& hp, gen::GenParams& gp) {
     gp.sg.l4_off[f] = rb ? hp.l4_offset[f] : hp.l4_offset[f] >> 3;
     gp.sg.l4_m[f] = x4.m;
     gp.sg.l4_xs[f] = x4.xs;
-    std::memcpy(gp.sg.l4_w[f], &hp.l4_weight[(size_t)f * F2], 16);
-    // layer 3: torch-order taps W3t[j] = net_l3_weight[f][15 - j] (stored flipped); output phase k
-    // of a 4-output group meets window byte q with tap q - k - 1
-    for (int k = 0; k < 4; k++) {
-      int8_t w[32] = {0};
-      for (int q = 0; q < 20; q++) {
-        const int j = q - k - 1;
-        w[q] = (j >= 0 && j < 16) ? hp.l3_weight[(size_t)f * 16 + 15 - j] : 0;
-      }
-      std::memcpy(gp.sg.l3_w[f][k], w, 32);
-    }
   }
+  // layer 4 (gen::layer4): lane (column c = lane & 31, K half h = lane >> 5) holds B[16 h .. +15][c]
+  // = W4[c & 15][0 .. 15] when h == c >> 4, else zeros
+  for (int lane = 0; lane < 64; lane++) {
+    const int c = lane & 31, h = lane >> 5;
+    int8_t bytes[16] = {0};
+    if (h == (c >> 4)) std::memcpy(bytes, &hp.l4_weight[(size_t)(c & 15) * F2], 16);
+    std::memcpy(&gp.sg.l4_b[lane], bytes, 16);
+  }
+  // layer 3 (gen::layer3): torch-order taps W3t[t] = net_l3_weight[f][15 - t] (stored flipped).  Wave
+  // w's A fragment, lane (row r = lane & 15, K group kg = lane >> 4): K-slots 16 (kg & 1) .. +15 of
+  // filter 2w + (kg >> 1)'s 32-byte window, A[r][k] = W3t[k - r - 1]
+  for (int w = 0; w < gen::NW; w++)
+    for (int lane = 0; lane < 64; lane++) {
+      const int r = lane & 15, kg = lane >> 4, f = 2 * w + (kg >> 1);
+      int8_t bytes[16];
+      for (int jj = 0; jj < 16; jj++) {
+        const int t = 16 * (kg & 1) + jj - r - 1;
+        bytes[jj] = (t >= 0 && t < 16) ? hp.l3_weight[(size_t)f * 16 + 15 - t] : 0;
+      }
+      std::memcpy(&gp.sg.l3_a[w][lane], bytes, 16);
+    }
   l2_bands(hp, 1, gp.l2_a);
   // tail bands (gen::layer2): lane (shift m = lane & 15, g) of K-step s holds K-slots
   // 64 s + 16 g .. +15, window position k of the column meets tap k - m - 1
