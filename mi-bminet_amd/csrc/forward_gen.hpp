@@ -78,7 +78,9 @@ struct GenParams {
   int l5_xs;
   float l3_r, l3_c;             // float form of layer 3: magic C-init, fma(acc bits, r, c)
   int pad1[2];
-  v4i l1_b[64];                 // layer-1 B operand: lane (filter lane & 15, g) = W1[f][16 g .. +15]
+  v4i l1_b[64];                 // layer-1 B operand, time-major: lane (filter lane & 15, g) = W1[f] chunk
+                                // l1_chunk(g, C) (zero in K groups 1 and 3 when C <= 32)
+  v4i l1_bn[64];                // the same in natural order (channel-major, float32): chunk g
   int l1_off[F2];               // XR: offset (the MFMA C-init); float: offset + FMAGIC_I
   unsigned l1_m[F2];            // XR: xdiv magic
   int l1_xs[F2];
@@ -176,6 +178,13 @@ __device__ __forceinline__ View trial_view(const int8_t* x, long long b, int C, 
   return v;
 }
 
+// Time-major K groups: with C <= 32 channels 0..15 go to K group 0 and 16..31 to K group 2, and
+// groups 1 and 3 (zero weights) re-read the same 16 bytes.  A ds_read_b32 serves lanes 0-31 and
+// 32-63 in separate cycles, so each cycle then reads only 16 distinct windows, whose dwords
+// (5.5 j apart at C = 22) fall on distinct banks; groups 0 and 1 together, 16 bytes apart, met
+// 2-way conflicts (profiles/r06_lds_conflicts.txt).
+__host__ __device__ inline int l1_chunk(int g, int C) { return C <= 32 ? g >> 1 : g; }
+
 // The A fragment of layer-1 block blk (samples 16 blk .. +15), before staging: time-major, lane
 // (j, g) holds channels 16 g .. +15 of sample 16 blk + j; channel-major, lane c holds samples
 // 16 blk .. +15 of channel c.  K-slots past C meet zero weights, so what those lanes read does not
@@ -185,7 +194,7 @@ template <int L>
 __device__ __forceinline__ v4i l1_fetch(const View& v, int blk, int C, int T, int lane, float qs, float qy) {
   if constexpr (L == TM) {
     const int j = lane & 15, g = lane >> 4;
-    return load16u(v.r, v.delta + (16 * blk + j) * C + 16 * g);
+    return load16u(v.r, v.delta + (16 * blk + j) * C + 16 * l1_chunk(g, C));
   } else if constexpr (L == CT) {
     return load16u(v.r, v.delta + min(lane, C - 1) * T + 16 * blk);
   } else {
@@ -235,7 +244,7 @@ struct L1Src {
 };
 template <int L>
 __device__ __forceinline__ L1Src l1_src(const int8_t* raw, int delta, int C, int T, int lane) {
-  const int lb = L == TM ? delta + (lane & 15) * C + 16 * (lane >> 4) : delta + min(lane, C - 1) * T;
+  const int lb = L == TM ? delta + (lane & 15) * C + 16 * l1_chunk(lane >> 4, C) : delta + min(lane, C - 1) * T;
   return L1Src{raw + (lb & ~3), L == TM ? 16 * C : 16, (unsigned)(lb & 3)};
 }
 template <bool AL>
@@ -611,6 +620,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   L1C k1;
   L2C k2;
   setup(gp, smem, cv, k1, k2, tid, wave, lane);
+  if constexpr (L != TM) k1.wf = gp->l1_bn[lane];  // channel-major fragments keep the natural K order
   const SmallG* sg = (const SmallG*)(smem + cv.sg);
   int8_t* y1 = smem;
   int8_t* y2 = smem + cv.y2;

@@ -754,16 +754,21 @@ int build_genparams(HostParams& hp, gen::GenParams& gp) {
   gp.rb = hp.reorder_bn ? 1 : 0;
   gp.lo = hp.clip_balanced ? -127 : -128;
   gp.xstride = (int)(((size_t)C * d.T + 15) / 16 * 16);
-  // layer 1: lane (filter j, K group g) holds channels 16 g .. 16 g + 15 (zero past C)
+  // layer 1: lane (filter j, K group g) holds channels 16 c .. 16 c + 15 (zero past C) of chunk c:
+  // time-major c = gen::l1_chunk(g, C), zero in K groups 1 and 3 when C <= 32 (their lanes re-read
+  // the previous group's bytes); natural order (channel-major, float32) c = g
   for (int lane = 0; lane < 64; lane++) {
     const int j = lane & 15, g = lane >> 4;
-    int8_t bytes[16];
+    int8_t bytes[16], nat[16];
     for (int i = 0; i < 16; i++) {
-      const int c = 16 * g + i;
-      bytes[i] = c < C ? hp.l1_weight_align[(size_t)j * CA + c] : 0;
+      const int c = 16 * gen::l1_chunk(g, C) + i, cn = 16 * g + i;
+      bytes[i] = (c < C && !(C <= 32 && (g & 1))) ? hp.l1_weight_align[(size_t)j * CA + c] : 0;
+      nat[i] = cn < C ? hp.l1_weight_align[(size_t)j * CA + cn] : 0;
     }
     std::memcpy(&gp.l1_b[lane], bytes, 16);
+    std::memcpy(&gp.l1_bn[lane], nat, 16);
   }
+
   for (int f = 0; f < F2; f++) {
     const XDiv x1 = xdiv_consts(hp.l1_factor[f]);
     gp.l1_off[f] = hp.l1_offset[f];
