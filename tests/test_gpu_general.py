@@ -79,6 +79,10 @@ def test_channel_selected_few_class(C, N, T, gpu):
     (19, 480, 3, dict(reorder_bn=False)), (38, 1125, 2, dict(clip_balanced=True)),
     (16, 777, 3, dict(weight_bits=4)), (13, 640, 2, dict(stress=True)),
     (38, 480, 2, dict(stress=True, reorder_bn=False, clip_balanced=True)),
+    # the time-major K-group layouts: C <= 32 uses K groups 0 and 2 (16-byte-aligned fragments at
+    # C = 16, 32), 32 < C <= 64 all four (aligned at 48)
+    (32, 1125, 4, {}), (17, 480, 3, {}), (24, 512, 2, {}), (31, 1000, 4, dict(reorder_bn=False)),
+    (48, 960, 4, {}), (40, 1125, 3, dict(clip_balanced=True)),
 ])
 def test_other_geometries_and_variants(C, T, N, kw, gpu):
     """Odd and extreme T (1 pooled layer-4 sample at T = 64, the 4096-sample maximum), one and
