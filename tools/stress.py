@@ -39,7 +39,10 @@ def main():
     ap.add_argument("--B", type=int, default=65536)
     ap.add_argument("--nb", type=int, default=8, help="distinct input batches per parameter mode")
     ap.add_argument("--layout", default="tc", choices=("tc", "ct", "f32"))
-    ap.add_argument("--cfg", default="b22", choices=("b22", "c64", "p64"), help="geometry of the batch stress")
+    ap.add_argument("--cfg", default="b22", choices=("b22", "c64", "p64", "g19", "g38", "p64l"),
+                    help="geometry of the batch stress (g19 / g38 / p64l: the general kernels)")
+    ap.add_argument("--force-general", action="store_true",
+                    help="run the compiled geometries on the general kernels (mibminet_test_force_general)")
     ap.add_argument("--variants", default="canonical",
                     help="comma list of build variants to stress: canonical, plain_bn, clip_balanced")
     ap.add_argument("--extreme", action="store_true",
@@ -47,6 +50,8 @@ def main():
     a = ap.parse_args()
     if a.lib:
         lib.load(os.path.abspath(a.lib))
+    if a.force_general:
+        lib.force_general(True)
     f = np.load(os.path.join(ROOT, "tests/golden/fixture_b22_stress.npz"))
     ps = ParamSet.from_blob(f["blob"].tobytes())
     lib.params_load(ps)
@@ -65,13 +70,14 @@ def main():
 
     modes = [(v, st) for v in a.variants.split(",") for st in ((False,) if a.extreme else (True, False))]
     for variant, stress in modes:
-        gC, gT = {"b22": (22, 1125), "c64": (64, 1000), "p64": (64, 480)}[a.cfg]
+        gC, gT, gN = {"b22": (22, 1125, 4), "c64": (64, 1000, 4), "p64": (64, 480, 4), "g19": (19, 1125, 3),
+                      "g38": (38, 480, 2), "p64l": (64, 960, 4)}[a.cfg]
         if a.extreme:
             ps = ParamSet.synthetic_extreme(7, reorder_bn=variant != "plain_bn",
-                                            clip_balanced=variant == "clip_balanced", C=gC, T=gT)
+                                            clip_balanced=variant == "clip_balanced", C=gC, T=gT, N=gN)
         else:
             ps = ParamSet.synthetic(seed=7, stress=stress, reorder_bn=variant != "plain_bn",
-                                    clip_balanced=variant == "clip_balanced", C=gC, T=gT)
+                                    clip_balanced=variant == "clip_balanced", C=gC, T=gT, N=gN)
         lib.params_load(ps)
         stride = lib.trial_stride()
         g = torch.Generator(device="cuda:0").manual_seed(11 + stress)
@@ -98,7 +104,7 @@ def main():
             del x
         print(f"oracle on {a.nb} x {a.B} trials: {time.time() - t0:.1f} s", flush=True)
         xp = torch.empty_like(xs[0])
-        y = torch.empty((a.B, 4), dtype=torch.int8, device="cuda:0")
+        y = torch.empty((a.B, ps.dims.N), dtype=torch.int8, device="cuda:0")
         bad2 = 0
         t0 = time.time()
         for i in range(a.n2):
@@ -122,7 +128,7 @@ def main():
                 if bad2 <= 5:
                     rows = torch.nonzero(bad).flatten()[:4].tolist()
                     print(f"batch launch {i}: {nb} trials differ, first {rows}", flush=True)
-        print(f"batch ({a.layout}, {a.cfg}, {variant}, {'extreme' if a.extreme else f'stress={stress}'}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
+        print(f"batch ({a.layout}, {a.cfg}{' general' if a.force_general or a.cfg[0] == 'g' or a.cfg == 'p64l' else ''}, {variant}, {'extreme' if a.extreme else f'stress={stress}'}): {bad2} of {a.n2} launches wrong, {a.n2 * a.B:.3g} trials checked, "
               f"{a.nb * a.B} distinct ({time.time() - t0:.1f} s)", flush=True)
 
 if __name__ == "__main__":
