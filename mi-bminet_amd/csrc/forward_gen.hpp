@@ -10,24 +10,27 @@
 // their compile-time specialisations (forward_wg.hpp), which this file does not touch.
 //
 // One workgroup of NW = 8 wave64s owns one trial at a time (persistent, grid-strided), with two
-// barriers per trial: waves 0-6 run layer 1 while wave 7 runs layers 4-5 of the previous trial.
-// Int8 trials arrive in LDS a trial ahead by LDS-DMA.  Every intermediate stays in LDS:
+// barriers per trial: waves 0-6 run layer 1 while wave 7 runs layers 4-5 of the previous trial
+// and then the trial's last K7 layer-1 blocks.  Int8 trials arrive in LDS a trial ahead by
+// LDS-DMA.  Every intermediate stays in LDS:
 //   layer1  MFMA i32_16x16x64_i8: A = 16 samples x 64 channel slots, B = the 16 filters' weights
 //           (zero past C), C-init = the offset.  Time-major trials: a lane's 16 bytes of sample
-//           t are t C + 16 g .. +15 of the trial, read as five aligned dwords and realigned by
-//           v_alignbyte (no load straddles the view, so no byte is lost to the per-dword range
-//           check); channel-major trials (int8 or float32, quantised here) go through the same
-//           LDS transpose as the specialised kernels (wg::stage_block, ds_read_b64_tr_b8).
+//           t are t C + 16 c .. +15 of the trial (chunk c = l1_chunk(g, C)), read as five aligned
+//           dwords and realigned by v_alignbyte (one ds_read_b128 when every fragment is
+//           16-byte aligned); channel-major trials (int8 or float32, quantised here) go through
+//           the same LDS transpose as the specialised kernels (wg::stage_block, ds_read_b64_tr_b8).
 //                                                               (reference: layer1.c:53-101)
 //   layer2  the 64-tap depthwise xcorr as a banded-Toeplitz GEMM on MFMA i32_32x32x32_i8 (A = 32
 //           output shifts x 96-tap band, rows permuted so that a lane holds two whole pool-8
 //           windows; B = 16-byte slices of the layer-1 row), ReLU-pool and requant per lane.
 //                                                               (reference: layer2.c:56-118, 139-210)
-//   layer3  16-tap depthwise conv on the VALU: four outputs per lane from five aligned dwords of
-//           the layer-2 row against four pre-shifted tap vectors (v_dot4_i32_i8), written
-//           transposed [u][f] (the reference's flip is index math).   (reference: layer3.c:49-79)
-//   layer4  16x16 pointwise on the VALU (v_dot4), ReLU-pool and requant.  (reference: layer4.c:51-149)
-//   layer5  N-class linear layer: one wave per class, v_dot4 + a wave reduction.  (reference: layer5.c:43-89)
+//   layer3  16-tap depthwise conv on MFMA i32_16x16x64_i8 with a block-diagonal K (the wave's two
+//           filters), written transposed [u][f] (the reference's flip is index math).
+//                                                               (reference: layer3.c:49-79)
+//   layer4  16x16 pointwise on MFMA i32_32x32x32_i8 with a block-diagonal B (two 32-sample
+//           blocks), ReLU-pool and requant per lane.               (reference: layer4.c:51-149)
+//   layer5  N-class linear layer: four classes per pass, 16 lanes each, v_dot4 + a DPP prefix.
+//                                                               (reference: layer5.c:43-89)
 // Requantisation as in the compiled kernels: where the host proves the float form exact on every
 // reachable value (mibminet.hip: choose_reciprocal, choose_floor_form) the XR = false build runs
 // it; any requant without a proven float form sends the set to the XR = true build, exact
@@ -123,7 +126,7 @@ __host__ __device__ inline Carve carve_of(int C, int T, int N, int T8, int T64A,
   c.y2s = align16(T8 + 32);     // 8 pad bytes, T8 outputs, zeros under layer 3's 20-byte windows
   c.y2 = 16 * c.y1s;
   c.y3 = c.y2 + 16 * c.y2s;
-  c.y4 = c.y3 + align16(16 * (T8 + 3));       // layer 3 stores rows up to T8 + 2 unconditionally
+  c.y4 = c.y3 + align16(16 * (T8 + 3));       // rows < T8 (layer 3), zeros past them
   c.sg = c.y4 + w5_row(T64A);                 // y4 padded with zeros to whole 256-byte rows
   c.w5 = c.sg + (int)sizeof(SmallG);          // layer-5 weights [N][w5_row], then the N biases
   c.stg = c.w5 + N * w5_row(T64A) + align16(4 * N);  // channel-major transpose staging, 1 KB per wave
