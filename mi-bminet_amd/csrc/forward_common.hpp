@@ -200,7 +200,7 @@ struct L1Tile {
   v4i wf;
   int ci;
   float rr, cc;      // float requant: reciprocal and magic constant
-  unsigned xm;       // XR: xdiv magic and shift word, carried as integers (never in a float)
+  unsigned xm;       // XR: the xdiv constant's low and high words, carried as integers
   int xs;
 };
 
@@ -217,17 +217,18 @@ __device__ __forceinline__ f2 fma2(int a, int b, float r, float c) {
 __device__ __forceinline__ f2 mul2(float a, float b, float r) { return (f2){a * r, b * r}; }
 
 // Exact C division trunc(e / d) for every int32 e and d != 0 (the reference's int32 division;
-// INT_MIN / -1 is refused at load), for the exact-division builds (Cfg::XR).  m and xs come from
-// the host (mibminet.hip, xdiv_consts: m = ceil(2^(31 + l) / |d|), l = ceil(log2 |d|), xs = l |
-// sign(d) << 31): floor(|e| / |d|) is bits 31 .. 62 of the 64-bit product |e| m shifted right by
-// l (v_mad_u64_u32, v_alignbit_b32, v_lshrrev_b32; the shift uses bits 0-4 of xs), then the sign
-// of e / d is restored.  Proof and host emulation: mibminet.hip; tests/test_xdiv.py.
-__device__ __forceinline__ int xdiv(int e, unsigned m, int xs) {
-  const int es = e >> 31;
-  const unsigned x = (unsigned)((e ^ es) - es);  // |e|, 2^31 for INT_MIN
-  const unsigned q = (unsigned)(((unsigned long long)x * m) >> 31) >> (xs & 31);
-  const int sg = (e ^ xs) >> 31;                  // the quotient is negative
-  return (int)((q ^ (unsigned)sg) - (unsigned)sg);
+// INT_MIN / -1 is refused at load), for the exact-division builds (Cfg::XR).  (lo, hi) are the two
+// halves of the double r = sign(d) RU(1 / |d|) (mibminet.hip, xdiv_consts): trunc(e r) in double
+// (v_cvt_f64_i32, v_mul_f64, v_cvt_i32_f64) equals trunc(e / d).  For e, d > 0 with e / d = q + f:
+// e r >= e / d, so the rounded product is >= q; e r - e / d <= e 2^-52 / d, and the distance from
+// q + f to q + 1 is >= 1 / d > 1.5 (e / d) 2^-52 for |e| <= 2^31, more than the error plus half an
+// ulp of the product, so it stays below q + 1.  The other signs are the mirror image.  Proof and
+// host emulation: mibminet.hip, xdiv_consts / xdiv_host; every int32 dividend on the device for
+// three divisors and every quotient step for many more: tests/test_gpu_xr.py.  (Round 5 used a
+// 32 x 32 -> 64-bit integer multiply-shift, about twice the issue cycles.)
+__device__ __forceinline__ int xdiv(int e, unsigned lo, int hi) {
+  const double r = __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | lo);
+  return (int)((double)e * r);
 }
 
 // max(a, thr) - thr for a biased accumulator value acc = a + B and thrb = thr + B

@@ -231,26 +231,30 @@ bool choose_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* mbits, 
 // (Granlund & Montgomery's round-up method with one spare bit of multiplier.)  The device takes
 // x = |e| as a u32 (2^31 for INT_MIN), the 64-bit product x m, its bits 31 .. 62 and a shift by
 // l, then restores the sign of e / d.  xs packs l (bits 0-4) and the sign of d (bit 31).
+// Exact division constants (forward_common.hpp, xdiv): the double r = sign(d) RU(1 / |d|), split
+// into its low word (m) and high word (xs).  RU: 1 / |d| rounded to nearest, then one ulp up when
+// that fell below (the fma residual r |d| - 1 is exact in sign).  Powers of two are exact.
 struct XDiv {
   uint32_t m;
   int32_t xs;
 };
 
 XDiv xdiv_consts(int32_t d) {
-  const uint64_t D = d < 0 ? (uint64_t)(-(int64_t)d) : (uint64_t)d;
-  int l = 0;
-  while (((uint64_t)1 << l) < D) l++;
-  const uint64_t m = (((uint64_t)1 << (31 + l)) + D - 1) / D;
-  return XDiv{(uint32_t)m, (int32_t)((uint32_t)l | (d < 0 ? 0x80000000u : 0u))};
+  const double D = std::fabs((double)d);
+  double r = 1.0 / D;
+  if (std::fma(r, D, -1.0) < 0.0) r = std::nextafter(r, INFINITY);
+  if (d < 0) r = -r;
+  uint64_t bits;
+  std::memcpy(&bits, &r, 8);
+  return XDiv{(uint32_t)bits, (int32_t)(uint32_t)(bits >> 32)};
 }
 
-// the device sequence of xdiv on the host (mibminet_test_xdiv)
+// the device sequence of xdiv on the host (mibminet_test_xdiv): IEEE double product, truncation
 int32_t xdiv_host(int32_t e, XDiv c) {
-  const int32_t es = e >> 31;
-  const uint32_t x = (uint32_t)((e ^ es) - es);
-  const uint32_t q = (uint32_t)(((uint64_t)x * c.m) >> 31) >> (c.xs & 31);
-  const int32_t sg = (e ^ c.xs) >> 31;
-  return (int32_t)((q ^ (uint32_t)sg) - (uint32_t)sg);
+  const uint64_t bits = ((uint64_t)(uint32_t)c.xs << 32) | c.m;
+  double r;
+  std::memcpy(&r, &bits, 8);
+  return (int32_t)((double)e * r);
 }
 
 // Reachable range of an int8 dot product sum_i w[i] x[i] over inputs x in [-128, 127] (every
