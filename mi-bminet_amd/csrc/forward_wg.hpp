@@ -742,7 +742,11 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
 #pragma unroll
   for (int t = 0; t < K::P; t++) {  // both N-tiles' MFMAs before either requant
     const L1Tile& T = R.tile(t);
-    accs[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, T.wf, (v4i){T.ci, T.ci, T.ci, T.ci}, 0, 0, 0);
+    // XR: the inline constant 0, the offset added before the division (a register C-init tuple
+    // per tile did not stay resident beside the division's double temporaries, and its rebuild
+    // inside the loop is the pattern tools/cinit_scan.py forbids)
+    const int ci = K::XR ? 0 : T.ci;
+    accs[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, T.wf, (v4i){ci, ci, ci, ci}, 0, 0, 0);
   }
 #pragma unroll
   for (int t = 0; t < K::P; t++) {
@@ -756,9 +760,9 @@ __device__ __forceinline__ void l1_block(v4i a, int blk, int8_t* smem_y1, const 
     const int t0 = K::PSPLIT ? 2 * (16 * blk + 4 * g) + p : K::P == 2 ? 32 * blk + 16 * p + 4 * g : 16 * blk + 4 * g;
     constexpr int SS = K::PL;  // sample stride of the lane's 4 outputs
     int y[4];
-    if constexpr (K::XR) {  // acc = dot + off (C-init = off): exact division
+    if constexpr (K::XR) {  // acc = dot (C-init 0): exact division of dot + off
 #pragma unroll
-      for (int r = 0; r < 4; r++) y[r] = xdiv(acc[r], T.xm, T.xs);
+      for (int r = 0; r < 4; r++) y[r] = xdiv(acc[r] + T.ci, T.xm, T.xs);
     } else {
       // acc bits = 1.5*2^23 + (dot + off) as f32; fma(x, r, -1.5*2^23*r) == RN((dot+off)*r)
       const f2 q01 = fma2(acc[0], acc[1], T.rr, T.cc);
