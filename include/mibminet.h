@@ -107,8 +107,8 @@ int net_params_load(const void* blob, size_t len);
 
 /* Which kernels the loaded set runs, for integrators who need to see a slower path coming:
  * info[0] = NET_PATH_FLOAT (compiled geometry, float requant proven exact on every reachable
- * value), NET_PATH_EXACT (compiled geometry, exact integer division at layers 1, 2 and 4: about
- * 1.5x the float kernels' time on 22 x 1125) or NET_PATH_GENERAL (run-time-dimension kernels,
+ * value), NET_PATH_EXACT (compiled geometry, exact division at layers 1, 2 and 4: about
+ * 1.1x the float kernels' time on 22 x 1125) or NET_PATH_GENERAL (run-time-dimension kernels,
  * float or exact requant as info[4] says); info[1] = the layer (1, 2 or 4) of the first requant that has no
  * proven float form (NET_PATH_EXACT), else 0; info[2] = its filter, else -1; info[3] = the
  * compiled geometry (0: 22 x 1125, 1: 64 x 1000, 2: 64 x 480), -1 on the general path; info[4] = 1

@@ -222,15 +222,15 @@ bool choose_floor_form(int32_t fac, int64_t emax, int64_t vmax, int32_t* mbits, 
 
 // ---- exact integer division (XR builds) ------------------------------------------------------
 // Parameter sets outside the float envelope above (large folded BN offsets, or factors whose
-// reciprocal window the check cannot prove) run the Cfg::XR kernels, which divide exactly in
-// integers (forward_common.hpp, xdiv): for d != 0 with D = |d| and l = ceil(log2 D),
-// m = ceil(2^(31 + l) / D) lies in [2^31, 2^32), and for every x in [0, 2^31]
-//   floor(x / D) = floor(x m / 2^(31 + l))
-// because x m / 2^(31 + l) = x / D + x e / (D 2^(31 + l)) with e = m D - 2^(31 + l) in [0, D), so
-// the error is below 2^31 D / (D 2^(31 + l)) = 2^-l <= 1 / D, and frac(x / D) <= (D - 1) / D.
-// (Granlund & Montgomery's round-up method with one spare bit of multiplier.)  The device takes
-// x = |e| as a u32 (2^31 for INT_MIN), the 64-bit product x m, its bits 31 .. 62 and a shift by
-// l, then restores the sign of e / d.  xs packs l (bits 0-4) and the sign of d (bit 31).
+// reciprocal window the check cannot prove) run the Cfg::XR kernels, which divide exactly
+// (forward_common.hpp, xdiv): trunc(e r) in IEEE double with r = sign(d) RU(1 / |d|) equals C's
+// trunc(e / d) for every int32 e.  For e, d > 0 with e / d = q + f (f a multiple of 1 / d,
+// f <= 1 - 1 / d): 0 <= e r - e / d <= e 2^-52 / d, so the exact product lies in
+// [q + f, q + f + e 2^-52 / d]; rounding it cannot go below q (q is a double), and its distance
+// from q + 1 is at least (1 - e 2^-52) / d, more than half an ulp of the product ((e / d) 2^-53)
+// for every e <= 2^31.  Negative e or d mirror it (the product changes sign only).  Round 5's
+// integer form (m = ceil(2^(31 + l) / |d|), a 32 x 32 -> 64 product and a shift) took about
+// twice the issue cycles.
 // Exact division constants (forward_common.hpp, xdiv): the double r = sign(d) RU(1 / |d|), split
 // into its low word (m) and high word (xs).  RU: 1 / |d| rounded to nearest, then one ulp up when
 // that fell below (the fma residual r |d| - 1 is exact in sign).  Powers of two are exact.
