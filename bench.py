@@ -375,7 +375,9 @@ def main():
         value = world * B * a.steps / elapsed
         out = {
             "metric": (METRIC if a.config == "b22" and a.variant == "canonical" and a.layout == "tc" and a.params == "synthetic"
+                       and not a.force_general
                        else f"EEG trials/sec ({cfg['name']}, {a.variant} build, {a.params} parameters, "
+                            f"{'general kernels, ' if a.force_general else ''}"
                             f"{ {'ct': 'channel-major', 'f32': 'float32 channel-major', 'tc': 'time-major'}[a.layout]} "
                             f"input) at batch {B}"),
             "value": value,
