@@ -34,7 +34,7 @@
 // Requantisation as in the compiled kernels: where the host proves the float form exact on every
 // reachable value (mibminet.hip: choose_reciprocal, choose_floor_form) the XR = false build runs
 // it; any requant without a proven float form sends the set to the XR = true build, exact
-// integer division (xdiv, forward_common.hpp) at layers 1-4.  Layer 5 always divides exactly (its
+// division (xdiv, forward_common.hpp) at layers 1-4.  Layer 5 always divides exactly (its
 // sums pass 2^24 at T = 4096).  CB: balanced clipping ([-127, 127], golden model clip_balanced).
 #pragma once
 #include "forward_wg.hpp"
@@ -189,7 +189,7 @@ __device__ __forceinline__ View trial_view(const int8_t* x, long long b, int C, 
 __host__ __device__ inline int l1_chunk(int g, int C) { return C <= 32 ? g >> 1 : g; }
 
 // The A fragment of layer-1 block blk (samples 16 blk .. +15), before staging: time-major, lane
-// (j, g) holds channels 16 g .. +15 of sample 16 blk + j; channel-major, lane c holds samples
+// (j, g) holds channels 16 c .. +15 (c = l1_chunk(g, C)) of sample 16 blk + j; channel-major, lane c holds samples
 // 16 blk .. +15 of channel c.  K-slots past C meet zero weights, so what those lanes read does not
 // matter: the loads are unconditional (no per-lane branch between one block's loads and the next
 // block's), and channel-major rows past C re-read row C - 1.
@@ -235,7 +235,8 @@ __device__ __forceinline__ v4i lds16u(const int8_t* p, unsigned s) {
 }
 
 // A lane's layer-1 fragments in the staged trial: block blk's 16 bytes start at lb + step blk, with
-// lb = delta + j C + 16 g (time-major) or delta + c T (channel-major, c = min(lane, C - 1)) and
+// lb = delta + j C + 16 l1_chunk(g, C) (time-major) or delta + c T (channel-major, c = min(lane,
+// C - 1)) and
 // step = 16 C or 16.  step is a multiple of 4, so the byte shift lb & 3 is the same for every block
 // and each block costs one address add.  AL: every fragment 16-byte aligned (delta = 0 and the row
 // length a multiple of 16), one ds_read_b128 each; otherwise lds16u (at C = 64 its five dwords per
