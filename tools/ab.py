@@ -31,11 +31,15 @@ def main():
     ap.add_argument("--ct", action="store_true", help="channel-major input (net_model_compute_batch_ct)")
     ap.add_argument("--f32", action="store_true", help="float32 channel-major input (net_model_compute_batch_f32)")
     ap.add_argument("--extreme", action="store_true", help="ParamSet.synthetic_extreme (the exact-division kernels)")
+    ap.add_argument("--force-general", action="store_true",
+                    help="run the compiled geometries on the general kernels (mibminet_test_force_general)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
-    C, T = {"b22": (22, 1125), "c64": (64, 1000), "p64": (64, 480)}[a.cfg]
+    C, T, N = {"b22": (22, 1125, 4), "c64": (64, 1000, 4), "p64": (64, 480, 4), "g19": (19, 1125, 3),
+               "g38": (38, 480, 2), "g16": (16, 1125, 4), "g32": (32, 960, 2), "p64l": (64, 960, 4)}[a.cfg]
     mk = ParamSet.synthetic_extreme if a.extreme else ParamSet.synthetic
-    blob = mk(1, C=C, T=T, reorder_bn=a.variant != "plain_bn", clip_balanced=a.variant == "clip_balanced").to_blob()
+    blob = mk(1, C=C, T=T, N=N, reorder_bn=a.variant != "plain_bn",
+              clip_balanced=a.variant == "clip_balanced").to_blob()
     libs = []
     for p in a.libs:
         L = ctypes.CDLL(os.path.abspath(p), mode=ctypes.RTLD_LOCAL)
@@ -51,6 +55,8 @@ def main():
             f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_float, ctypes.c_int,
                           ctypes.c_void_p]
             L.net_model_compute_batch_async = (lambda f: lambda x, y, B, d, s: f(x, y, B, 3.0, d, s))(f)
+        if a.force_general:
+            L.mibminet_test_force_general(1)
         rc = L.net_params_load(blob, len(blob))
         assert rc == 0, (p, rc)
         libs.append(L)
@@ -59,7 +65,7 @@ def main():
         x = torch.randn((a.B, C, T), dtype=torch.float32, device="cuda:0")
     else:
         x = torch.randint(-128, 128, (a.B, stride), dtype=torch.int8, device="cuda:0")
-    y = torch.empty((a.B, 4), dtype=torch.int8, device="cuda:0")
+    y = torch.empty((a.B, N), dtype=torch.int8, device="cuda:0")
     st = torch.cuda.current_stream()
     outs = []
     for L in libs:
