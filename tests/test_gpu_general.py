@@ -102,6 +102,59 @@ def test_extreme_requant_sets(C, T, gpu):
         assert lib.params_info()["exact_division"]
 
 
+def _tile_sweep():
+    """32 geometries, one per residue of layer 2's column blocks mod 32 (NB2 = ceil(T8 / 4): rest
+    0 = whole 32x32 tiles, 1-16 = one or two 16x16x64 tail tiles, 17-31 = one more full tile),
+    each with 0-4 full tiles, C over 1..64, N over 1..16, T mod 16 and T mod 64 varied, the
+    largest trials past the LDS staging limit (unstaged fragments), and both build variants on
+    some of them."""
+    out = []
+    for rest in range(32):
+        m = max(rest % 4, 1 if rest < 2 else 0)
+        T8 = 4 * (32 * m + rest) - rest % 4
+        T = 8 * T8 + (3 * rest) % 8
+        kw = {}
+        if rest % 5 == 1:
+            kw["reorder_bn"] = False
+        if rest % 7 == 3:
+            kw["clip_balanced"] = True
+        out.append((1 + (7 * rest) % 64, T, 1 + rest % 16, kw))
+    return out
+
+
+@pytest.mark.parametrize("C,T,N,kw", _tile_sweep())
+def test_layer2_tile_sweep(C, T, N, kw, gpu):
+    """Every layer-2 tile residue (full and tail tiles), against the oracle through the batched
+    time-major and channel-major entries and the single-trial net_model_compute."""
+    assert 64 <= T <= 4096
+    ps = ParamSet.synthetic(seed=7 * C + T + N, C=C, T=T, N=N, **kw)
+    _check_all_entries(ps, B=7, seed=C * N, offset=2, layers=False)
+
+
+def _random_geometries(n=256, seed=20261018):
+    """n geometries drawn over the whole accepted domain (C 1..64, T 64..4096, N 1..16, both BN
+    branches, both clips, int8 or int4 weights), seeded; compiled shapes drawn are kept (they run
+    the general kernels only when forced, which test_compiled_geometries_forced_general covers)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    while len(out) < n:
+        C, T, N = int(rng.integers(1, 65)), int(rng.integers(64, 4097)), int(rng.integers(1, 17))
+        if (C, T, N) in ((22, 1125, 4), (64, 1000, 4), (64, 480, 4)):
+            continue
+        kw = dict(reorder_bn=bool(rng.integers(0, 4)), clip_balanced=not rng.integers(0, 4),
+                  weight_bits=4 if not rng.integers(0, 6) else 8)
+        out.append((C, T, N, kw))
+    return out
+
+
+@pytest.mark.parametrize("C,T,N,kw", _random_geometries())
+def test_random_geometries(C, T, N, kw, gpu):
+    """Seeded draws over the accepted domain, batched time-major and channel-major and the
+    single-trial entry against the oracle."""
+    ps = ParamSet.synthetic(seed=C * 4099 + T * 17 + N, C=C, T=T, N=N, **kw)
+    _check_all_entries(ps, B=5, seed=C + T, offset=T % 4, layers=False)
+
+
 def test_float_input_general(gpu):
     """net_model_compute_batch_f32 on a general geometry equals the two-pass chain (the quantiser,
     itself checked on every float32 value, then the time-major forward) and the oracle."""
