@@ -155,6 +155,26 @@ def test_random_geometries(C, T, N, kw, gpu):
     _check_all_entries(ps, B=5, seed=C + T, offset=T % 4, layers=False)
 
 
+def _random_extreme(n=48, seed=31337):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        C, T, N = int(rng.integers(1, 65)), int(rng.integers(64, 4097)), int(rng.integers(1, 17))
+        out.append((C, T, N, dict(reorder_bn=bool(rng.integers(0, 2)), clip_balanced=bool(rng.integers(0, 2)),
+                                  mids=int(rng.choice([0, 1, 3, 11])))))
+    return out
+
+
+@pytest.mark.parametrize("C,T,N,kw", _random_extreme())
+def test_random_extreme_sets(C, T, N, kw, gpu):
+    """ParamSet.synthetic_extreme on seeded random geometries: with only constant out-of-envelope
+    filters (mids = 0) the folded set runs the float kernels, with varying ones the exact-division
+    kernels; both equal the oracle on the set as given."""
+    ps = ParamSet.synthetic_extreme(seed=C + 131 * T + N, C=C, T=T, N=N, **kw)
+    _check_all_entries(ps, B=5, seed=T, offset=1, layers=T <= 1200)
+    assert lib.params_info()["exact_division"] == (kw["mids"] > 0)
+
+
 def test_float_input_general(gpu):
     """net_model_compute_batch_f32 on a general geometry equals the two-pass chain (the quantiser,
     itself checked on every float32 value, then the time-major forward) and the oracle."""
