@@ -193,6 +193,22 @@ def test_float_input_general(gpu):
         np.testing.assert_array_equal(lib.forward_torch(q).cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("C,T,N,kw", _random_geometries(24, seed=4242))
+def test_random_geometries_float_input(C, T, N, kw, gpu):
+    """net_model_compute_batch_f32 (quantised inside the general kernel) on seeded random
+    geometries: equal to the quantiser followed by the time-major forward, and to the oracle."""
+    import torch
+
+    ps = ParamSet.synthetic(seed=C + 7 * T + N, C=C, T=T, N=N, **kw)
+    lib.params_load(ps)
+    g = torch.Generator(device="cuda").manual_seed(T)
+    xf = torch.randn((9, C, T), dtype=torch.float32, device="cuda", generator=g) * 1.7
+    q = lib.quantize_input_torch(xf, 3.0)
+    want = oracle.COracle(ps).batch(q.cpu().numpy(), nthreads=NTH)
+    np.testing.assert_array_equal(lib.forward_f32_torch(xf, 3.0).cpu().numpy(), want)
+    np.testing.assert_array_equal(lib.forward_torch(q).cpu().numpy(), want)
+
+
 @pytest.mark.parametrize("C,T,wbits,rb", [(22, 1125, 8, True), (64, 1000, 8, True), (64, 480, 8, False),
                                           (22, 1125, 4, True)])
 def test_compiled_geometries_forced_general(C, T, wbits, rb, gpu):
