@@ -295,14 +295,15 @@ struct L1C {  // a lane's layer-1 constants (filter lane & 15)
 };
 
 // ST: the trial is staged in LDS (sraw).  The U blocks' loads are all issued before the first MFMA
-// (slots past NB1 re-read the last block; their results are not stored).
-template <int L, bool ST, bool XR, bool CB>
+// (slots past NB1 re-read the last block; their results are not stored).  U4: four blocks per
+// group, else two (float32: always two).
+template <int L, bool ST, bool XR, bool CB, bool U4 = true>
 __device__ __forceinline__ void layer1(const GenParams* __restrict__ gp, const View& v, const int8_t* sraw, int8_t* y1,
                                        int y1s, int8_t* stg, const L1C& k, int first, int nw, int end, int lane,
                                        float qs, float qy) {
   const int C = gp->C, T = gp->T, NB1 = gp->NB1;
   const int j = lane & 15, g = lane >> 4;
-  constexpr int U = L == F32 ? 2 : 4;
+  constexpr int U = L == F32 || !U4 ? 2 : 4;
   // staged fragments all 16-byte aligned (wave-uniform: a scalar branch per group of U blocks)
   const bool al = ST && v.delta == 0 && ((L == TM ? C : T) & 15) == 0;
   const L1Src src = l1_src<L>(sraw, v.delta, C, T, lane);
@@ -632,6 +633,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   int8_t* y4 = smem + cv.y4;
   int8_t* stg = smem + cv.stg + 1024 * wave;
   const int C = gp->C, T = gp->T, N = gp->N, xstride = gp->xstride, NB1 = gp->NB1, K7 = gp->K7;
+  // layer-1 groups of two blocks when two workgroups share the CU (the other one's waves cover the
+  // latency; a wave's ~10 blocks then leave no slot re-reading the last block), of four at one
+  // workgroup per CU (general kernels)
+  const bool two_wg = cv.bytes <= LDS_2WG;
   // int8 trials staged in LDS (cv.raw >= 0, uniform): the first one now; after that each trial a
   // grid stride ahead, by LDS-DMA issued after barrier A (layer 1 has read the area) and waited for
   // before barrier B, so it lands during layers 2-3 and no wave waits on HBM in layer 1
@@ -657,7 +662,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
     // dependency chain of the interval and issue first; layer 1 ahead of the other workgroup's 2-3
     if (wave < NW - 1) {
       __builtin_amdgcn_s_setprio(wg::PRIO_L1);
-      layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, wave, NW - 1, NB1 - K7, lane, qs, qy);
+      if (two_wg) layer1<L, ST, XR, CB, false>(gp, v, sraw, y1, cv.y1s, stg, k1, wave, NW - 1, NB1 - K7, lane, qs, qy);
+      else layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, wave, NW - 1, NB1 - K7, lane, qs, qy);
     } else {
       if (bprev >= 0) {
         __builtin_amdgcn_s_setprio(wg::PRIO_L45);
@@ -668,7 +674,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
       // then the trial's last K7 layer-1 blocks (host-balanced against layers 4-5)
       if (K7 > 0) {
         __builtin_amdgcn_s_setprio(wg::PRIO_L1);
-        layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, NB1 - K7, 1, NB1, lane, qs, qy);
+        if (two_wg) layer1<L, ST, XR, CB, false>(gp, v, sraw, y1, cv.y1s, stg, k1, NB1 - K7, 1, NB1, lane, qs, qy);
+        else layer1<L, ST, XR, CB>(gp, v, sraw, y1, cv.y1s, stg, k1, NB1 - K7, 1, NB1, lane, qs, qy);
       }
     }
     __builtin_amdgcn_s_setprio(0);
