@@ -36,7 +36,8 @@ def main():
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     C, T, N = {"b22": (22, 1125, 4), "c64": (64, 1000, 4), "p64": (64, 480, 4), "g19": (19, 1125, 3),
-               "g38": (38, 480, 2), "g16": (16, 1125, 4), "g32": (32, 960, 2), "p64l": (64, 960, 4)}[a.cfg]
+               "g38": (38, 480, 2), "g16": (16, 1125, 4), "g32": (32, 960, 2), "p64l": (64, 960, 4),
+               "g64t": (64, 1125, 4), "g48l": (48, 2000, 3)}[a.cfg]
     mk = ParamSet.synthetic_extreme if a.extreme else ParamSet.synthetic
     blob = mk(1, C=C, T=T, N=N, reorder_bn=a.variant != "plain_bn",
               clip_balanced=a.variant == "clip_balanced").to_blob()
