@@ -72,7 +72,8 @@ struct GenParams {
   int T64, T64A, NB1, MT;       // NB1: layer-1 blocks of 16 samples; MT: full layer-2 tiles of 1024 outputs
   int NTT;                      // layer-2 tail tiles of 256 outputs per filter past the MT full tiles
   int K7;                       // layer-1 blocks of the last wave (its layers 4-5 first), the trial's last ones
-  int pad2[2];
+  int K7T1;                     // the same for time-major trials at one workgroup per CU
+  int pad2;
   int rb, lo, xstride, xr;      // REORDER_BN branches; lower clip bound; time-major trial stride;
                                 // exact division (no proven float form for some requant)
   unsigned l3_m;
@@ -632,11 +633,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4, 4))) void
   int8_t* y3 = smem + cv.y3;
   int8_t* y4 = smem + cv.y4;
   int8_t* stg = smem + cv.stg + 1024 * wave;
-  const int C = gp->C, T = gp->T, N = gp->N, xstride = gp->xstride, NB1 = gp->NB1, K7 = gp->K7;
   // layer-1 groups of two blocks when two workgroups share the CU (the other one's waves cover the
   // latency; a wave's ~10 blocks then leave no slot re-reading the last block), of four at one
   // workgroup per CU (general kernels)
   const bool two_wg = cv.bytes <= LDS_2WG;
+  const int C = gp->C, T = gp->T, N = gp->N, xstride = gp->xstride, NB1 = gp->NB1;
+  const int K7 = L == TM && !two_wg ? gp->K7T1 : gp->K7;
   // int8 trials staged in LDS (cv.raw >= 0, uniform): the first one now; after that each trial a
   // grid stride ahead, by LDS-DMA issued after barrier A (layer 1 has read the area) and waited for
   // before barrier B, so it lands during layers 2-3 and no wave waits on HBM in layer 1

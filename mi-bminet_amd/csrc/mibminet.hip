@@ -755,6 +755,9 @@ int build_genparams(HostParams& hp, gen::GenParams& gp) {
   // (NB1 - K7) / 7 = 2 NP + K7, NP = layer-4 parts
   const int NP = (T64 + 7) / 8;
   gp.K7 = std::max(0, (gp.NB1 - 14 * NP) / 8);
+  // time-major at one workgroup per CU: two fewer (same box: -0.9 ... -2.6 %; channel-major
+  // measured +1.5 % and keeps K7, profiles/r06_ab_k7.txt)
+  gp.K7T1 = std::max(0, gp.K7 - 2);
   gp.rb = hp.reorder_bn ? 1 : 0;
   gp.lo = hp.clip_balanced ? -127 : -128;
   gp.xstride = (int)(((size_t)C * d.T + 15) / 16 * 16);
